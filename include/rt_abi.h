@@ -1,0 +1,155 @@
+/*
+ * rt_abi.h -- C ABI of the MI355X-native TinyRaytracer render path (librt_mi355x.so).
+ *
+ * This is the drop-in seam for the reference's src/raytracer render loop
+ * (andreivasiliu/TinyRaytracerInRust).  The reference has no FFI; its seam is the
+ * `RayTracer` the scene parser fills and the GUI worker renders row by row.  Each
+ * entry point below names the reference interface it replaces (file:line under
+ * src/).  The Rust-side `extern "C"` block a maintainer would add is shown in
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *   - every function returns RT_OK (0) or a negative rt_status; none aborts;
+ *     rt_last_error() returns a thread-local message for the last failure;
+ *   - no torch / HIP types in signatures: plain pointers, sizes and an opaque
+ *     `void* stream` (a hipStream_t, NULL = the context's own stream);
+ *   - the library owns rt_scene / rt_ctx; the caller owns every output buffer;
+ *   - an rt_scene is immutable once uploaded and may be shared by threads; an
+ *     rt_ctx is used by one host thread at a time; distinct contexts may run
+ *     concurrently;
+ *   - matrices are row-major double[16] (MatrixTransformation::matrix,
+ *     transformation.rs:47-51); an rt_transformation carries the matrix AND the
+ *     separately-built inverse, exactly like the reference (the rotation "inverse"
+ *     is Rx(-x)Ry(-y)Rz(-z), not a true inverse: transformation.rs:149-159).
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+typedef enum rt_status {
+  RT_OK = 0,
+  RT_ERR_INVALID = -1,      /* bad argument / handle / range                         */
+  RT_ERR_PARSE = -2,        /* scene text does not parse (scene_loader.rs:35)         */
+  RT_ERR_EVAL = -3,         /* scene evaluation error (the reference panics)          */
+  RT_ERR_IO = -4,           /* texture file missing / undecodable                     */
+  RT_ERR_DEVICE = -5,       /* HIP error, no GPU, or kernel launch failure            */
+  RT_ERR_UNSUPPORTED = -6,  /* outside this build's limits (e.g. max_depth > 16)      */
+  RT_ERR_NOMEM = -7
+} rt_status;
+
+typedef enum rt_csg_op { RT_CSG_UNION = 0, RT_CSG_INTERSECTION = 1, RT_CSG_DIFFERENCE = 2 } rt_csg_op;
+
+typedef struct rt_transformation {   /* MatrixTransformation (transformation.rs:47-51) */
+  double matrix[16];
+  double inverse[16];
+} rt_transformation;
+
+typedef struct rt_material {         /* SolidColorMaterial / TexturedMaterial (material.rs:34-102) */
+  double color[4];                   /* r,g,b,a; ignored when texture >= 0                      */
+  int32_t texture;                   /* texture id from rt_scene_add_texture, or -1 (solid)     */
+  double reflectivity;
+  double transparency;
+} rt_material;
+
+typedef struct rt_scene rt_scene;    /* a RayTracer (raytracer.rs:21-35): objects, lights, camera */
+typedef struct rt_ctx rt_ctx;        /* per-device context: stream, device scene, scratch        */
+
+/* ---- library ---------------------------------------------------------------------------- */
+int rt_abi_version(void);
+const char* rt_last_error(void);
+
+/* ---- transformations (replace MatrixTransformation constructors, transformation.rs:104-205) */
+int rt_xform_identity(rt_transformation* out);                                   /* :104-113 */
+int rt_xform_translation(double x, double y, double z, rt_transformation* out);  /* :164-180 */
+int rt_xform_rotation(double x, double y, double z, rt_transformation* out);     /* :115-162 */
+int rt_xform_scaling(double x, double y, double z, rt_transformation* out);      /* :182-198 */
+/* self.compose_with(other): matrix = other.m * self.m, inverse = self.inv * other.inv (:200-205);
+ * TransformationStack::push_transformation(t) == compose(t, top) (:21-28). */
+int rt_xform_compose(const rt_transformation* self_, const rt_transformation* other,
+                     rt_transformation* out);
+
+/* ---- scene construction (the RayTracer the scene parser fills) ------------------------- */
+/* RayTracer::new_default(width, height): camera at (0,0,-100), max_depth 10 (raytracer.rs:38-70) */
+int rt_scene_new(uint32_t width, uint32_t height, rt_scene** out);
+/* RayTracer::add_test_objects: the always-present light (-10,30,-50) rgb .5 (raytracer.rs:125-129) */
+int rt_scene_add_test_objects(rt_scene* scene);
+/* Textures: RGBA8 row-major, as lodepng::decode32_file returns them (sceneparser/texture.rs:20-40).
+ * The pixels are copied.  Returns the texture id (>= 0) or a negative rt_status. */
+int rt_scene_add_texture(rt_scene* scene, uint32_t width, uint32_t height, const uint8_t* rgba8);
+/* Shapes (math_shapes.rs / csg.rs constructors as reached from Shape::to_rt_object,
+ * sceneparser/shape.rs:42-93).  Each returns a shape id (>= 0) or a negative rt_status.
+ * Shapes are immutable values; one id may be used in several objects / CSG nodes. */
+int rt_shape_sphere(rt_scene* scene, const rt_transformation* t, const double center[3], double radius); /* :28-39 */
+int rt_shape_cube(rt_scene* scene, const rt_transformation* t, const double center[3], double length);   /* :227-245 */
+int rt_shape_plane(rt_scene* scene, const rt_transformation* t, const double normal[3], double distance);/* :154-156 */
+/* CSG::new(a, b, op) (csg.rs:15-31).  The children's own RTObject materials never reach the
+ * shading (only the top-level object's material is read, raytracer.rs:170,190,237-238), so
+ * none is taken here. */
+int rt_shape_csg(rt_scene* scene, rt_csg_op op, int32_t a, int32_t b);
+/* RayTracer::add_object(RTObject::new(shape, material)) (raytracer.rs:309-311, rt_object.rs:13-20) */
+int rt_scene_add_object(rt_scene* scene, int32_t shape, const rt_material* material);
+/* RayTracer::add_light(PointLight::new(point, color, fade_distance)) (raytracer.rs:305-307) */
+int rt_scene_add_light(rt_scene* scene, const double point[3], const double color[4], double fade_distance);
+/* PerspectiveCamera::new(width, height, center, None, None, None) with the centre ALREADY in
+ * world space (raytracer.rs:289-299 applies the transform; the DSL applies it once before). */
+int rt_scene_set_camera(rt_scene* scene, const double center[3]);
+int rt_scene_set_max_depth(rt_scene* scene, int32_t max_depth);                  /* raytracer.rs:65 */
+/* Whole-scene front end: restates load_scene (scene_loader.rs:24-47) on a fresh
+ * new_default()+add_test_objects() RayTracer (debug_window.rs:53-62), with the global `time`
+ * set (time = frame / 300 in the reference GUI).  Texture paths resolve against asset_dir
+ * (NULL = CWD).  On RT_ERR_PARSE *out still receives the default scene (the reference prints
+ * the error and renders the empty scene, debug_window.rs:58-60); on other errors *out = NULL. */
+int rt_scene_compile(const char* scene_text, const char* asset_dir, double time,
+                     uint32_t width, uint32_t height, rt_scene** out);
+int rt_scene_info(const rt_scene* scene, int32_t* n_objects, int32_t* n_lights, int32_t* n_leaves,
+                  uint32_t* width, uint32_t* height);
+void rt_scene_free(rt_scene* scene);
+
+/* ---- device rendering (replaces RayTracer::get_pixel + DebugWindow::render_lines) ------ */
+int rt_device_count(int* count);
+int rt_ctx_create(int device, rt_ctx** out);
+/* Flatten the scene to its HBM layout and copy it (and its textures) to the device, once per
+ * scene.  The scene may be freed afterwards. */
+int rt_ctx_upload(rt_ctx* ctx, const rt_scene* scene);
+/* Render full-frame rows [y0, y1) -- the camera always uses the full (W, H), so tiles compose
+ * (debug_window.rs:74-87 with `line_range` = y0..y1, pixel (x, y) -> get_pixel(x as f64, y as
+ * f64)).  Output RGBA8, row (y - y0) at rgba8 + (y - y0) * row_stride_bytes; each channel is
+ * `(c * 255.0) as u8` (easy_pixbuf.rs:49-52), R,G,B,A order.  rgba8 may be a device pointer
+ * (written by the kernel on `stream`, asynchronously) or a host pointer (rendered into the
+ * context's scratch and copied back; synchronous).  max_depth < 0 uses the scene's. */
+int rt_render_rows(rt_ctx* ctx, uint32_t y0, uint32_t y1, int32_t max_depth,
+                   uint8_t* rgba8, size_t row_stride_bytes, void* stream);
+/* Same, pre-quantisation colours: 4 doubles per pixel (r,g,b,a) -- the `Vec<Color>` rows. */
+int rt_render_rows_f64(rt_ctx* ctx, uint32_t y0, uint32_t y1, int32_t max_depth,
+                       double* rgba_f64, size_t row_stride_bytes, void* stream);
+/* Arbitrary sample positions (the anti-aliaser's fractional get_pixel calls,
+ * antialiaser.rs:108-112): xy = n pairs of doubles, out = n x 4 doubles. Device or host. */
+int rt_render_points_f64(rt_ctx* ctx, const double* xy, size_t n, int32_t max_depth,
+                         double* rgba_f64, void* stream);
+/* Milliseconds of the last render launch on this context (HIP events on its stream). */
+int rt_ctx_last_kernel_ms(rt_ctx* ctx, float* ms);
+int rt_ctx_synchronize(rt_ctx* ctx);
+void rt_ctx_free(rt_ctx* ctx);
+
+/* ---- output ----------------------------------------------------------------------------- */
+/* PNG encoder for the headless driver (the reference has none; it only paints a cairo
+ * surface).  channels = 3 (RGB, alpha dropped) or 4. Host pointer. */
+int rt_write_png(const char* path, const uint8_t* rgba8, uint32_t width, uint32_t height,
+                 size_t row_stride_bytes, int channels);
+/* PNG decoder used for textures (lodepng::decode32_file equivalent). *pixels is malloc'd;
+ * release with rt_free_buffer. */
+int rt_read_png_rgba8(const char* path, uint8_t** pixels, uint32_t* width, uint32_t* height);
+void rt_free_buffer(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_ABI_H */

@@ -1,0 +1,698 @@
+// render_kernels.hip -- gfx950 (MI355X, CDNA4) kernels for the TinyRaytracer render path, and
+// the device-context half of the C ABI (rt_ctx_*, rt_render_*).
+//
+// One thread per pixel; each 64-lane wave owns an 8x8 pixel tile (coherent primary rays,
+// fewer divergent CSG/shade branches than a 64x1 row strip); a 256-thread workgroup is a 16x16
+// tile.  All arithmetic is IEEE f64 with NO contraction (Rust never fuses): the file is
+// compiled with -ffp-contract=off and the pragma below.  sqrt and division lower to correctly
+// rounded sequences on gfx950 (verified bit-exact against glibc, profiles/r01_libm_probe.txt);
+// acos/sin come from ocml and may differ from glibc by 1 ulp (DESIGN.md "Parity").
+//
+// The reference's recursion (get_ray_color calling itself for refraction and reflection,
+// raytracer.rs:242-280) becomes an explicit per-lane frame stack combined in the same
+// post-order: child colour C folds into its parent as in_range(A + in_range(C * w)) where
+// A = parent.intensify(1 - w) -- exactly the `final.intensify(1-w) + R.intensify(w)` of
+// raytracer.rs:256-257 / :278-279.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include "rt_blob.h"
+#include "scene.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr double EPS = RT_EPSILON;
+constexpr double PI_D = 3.14159265358979323846;   // std::f64::consts::PI
+
+struct V3 { double x, y, z; };
+struct Col { double r, g, b; };
+
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V3 scale(V3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ double len(V3 a) { return sqrt(dot(a, a)); }
+__device__ __forceinline__ V3 normalized(V3 a) { return scale(a, 1.0 / len(a)); }
+__device__ __forceinline__ V3 ld3(const double* p) { return {p[0], p[1], p[2]}; }
+// transform_vector (transformation.rs:53-59) with rows m[0..3], m[4..7], m[8..11]
+__device__ __forceinline__ V3 xf(const double* m, V3 v) {
+  return {m[0] * v.x + m[1] * v.y + m[2] * v.z + m[3],
+          m[4] * v.x + m[5] * v.y + m[6] * v.z + m[7],
+          m[8] * v.x + m[9] * v.y + m[10] * v.z + m[11]};
+}
+// color.rs:36-53: clamp each channel (NaN passes through)
+__device__ __forceinline__ double in_limit(double x) { return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x); }
+__device__ __forceinline__ Col in_range(double r, double g, double b) { return {in_limit(r), in_limit(g), in_limit(b)}; }
+__device__ __forceinline__ Col intensify(Col c, double k) { return in_range(c.r * k, c.g * k, c.b * k); }
+__device__ __forceinline__ Col cmul(Col a, Col b) { return in_range(a.r * b.r, a.g * b.g, a.b * b.b); }
+__device__ __forceinline__ Col cadd(Col a, Col b) { return in_range(a.r + b.r, a.g + b.g, a.b + b.b); }
+// `(c * 255.0) as u8` (easy_pixbuf.rs:49-52): saturating truncation, NaN -> 0
+__device__ __forceinline__ uint32_t to_u8(double c) {
+  double v = c * 255.0;
+  if (!(v > 0.0)) return 0u;
+  if (v >= 255.0) return 255u;
+  return (uint32_t)v;
+}
+
+// ------------------------------------------------------------------ primitives (math_shapes.rs)
+__device__ __forceinline__ bool on_plane(const double* pl, V3 q) {        // :162-164
+  return fabs(pl[0] * q.x + pl[1] * q.y + pl[2] * q.z + pl[3]) < EPS;
+}
+
+__device__ bool leaf_inside(const RtLeaf* L, V3 p) {
+  int k = L->kind;
+  if (k == RT_N_PLANE) return false;                                        // :186-188
+  V3 q = xf(L->inv, p);
+  if (k == RT_N_SPHERE) return len(sub(q, ld3(L->c))) <= L->r_eps;         // :70-74
+  return q.x <= L->hi[0] && q.x >= L->lo[0] && q.y <= L->hi[1] &&          // :319-328
+         q.y >= L->lo[1] && q.z <= L->hi[2] && q.z >= L->lo[2];
+}
+
+__device__ bool leaf_on_surface(const RtLeaf* L, V3 p) {
+  V3 q = xf(L->inv, p);
+  int k = L->kind;
+  if (k == RT_N_SPHERE) return fabs(len(sub(q, ld3(L->c))) - L->radius) < EPS;   // :76-80
+  if (k == RT_N_PLANE) return on_plane(L->pl[0], q);                            // :190-194
+  bool bx = L->lo_e[0] <= q.x && q.x <= L->hi_e[0];                              // :330-355
+  bool by = L->lo_e[1] <= q.y && q.y <= L->hi_e[1];
+  bool bz = L->lo_e[2] <= q.z && q.z <= L->hi_e[2];
+  if (by && bx && (on_plane(L->pl[0], q) || on_plane(L->pl[5], q))) return true;
+  if (bz && bx && (on_plane(L->pl[1], q) || on_plane(L->pl[4], q))) return true;
+  if (by && bz && (on_plane(L->pl[2], q) || on_plane(L->pl[3], q))) return true;
+  return false;
+}
+
+__device__ V3 leaf_normal(const RtLeaf* L, V3 p) {
+  int k = L->kind;
+  if (k == RT_N_PLANE) return ld3(L->pn[0]);                               // :182-184
+  V3 q = xf(L->inv, p);
+  if (k == RT_N_SPHERE) {                                                  // :64-68
+    V3 n = sub(q, ld3(L->c));
+    return normalized(sub(xf(L->mat, n), ld3(L->mat_o)));
+  }
+  for (int i = 0; i < 6; ++i)                                              // :292-317
+    if (on_plane(L->pl[i], q)) return ld3(L->pn[i]);
+  return {1.0, 1.0, 1.0};
+}
+
+// MathSphere::get_uv_coordinates (:82-114): the centre is subtracted BEFORE the inverse transform
+__device__ void sphere_uv(const RtLeaf* L, V3 p, double* u, double* v) {
+  V3 q = xf(L->inv, sub(p, ld3(L->c)));
+  q = scale(normalized(q), 1.0 - EPS);
+  double phi = acos(-((0.0 * q.x + 1.0 * q.y) + 0.0 * q.z));             // up = (0,1,0)
+  if (isnan(phi)) phi = 0.0;
+  double theta = (acos(((q.x * 0.0 + q.y * 0.0) + q.z * -1.0) / sin(phi))) / (2.0 * PI_D);   // u_zero = (0,0,-1)
+  if (isnan(theta)) theta = 0.0;
+  *v = phi / PI_D;
+  *u = ((-1.0 * q.x + 0.0 * q.y) + 0.0 * q.z > 0.0) ? 1.0 - theta : theta;  // u_qrtr = (-1,0,0)
+}
+
+// Candidate hit distances of one primitive for the world ray (ro, rd):
+// RTObject::intersects (rt_object.rs:28-31) = reverse_transform_ray + MathShape::intersects.
+__device__ __forceinline__ int leaf_candidates(const RtLeaf* L, V3 ro, V3 rd, double* t0, double* t1) {
+  V3 o = xf(L->inv, ro);                                                   // transformation.rs:88-93
+  V3 d = sub(xf(L->inv, rd), ld3(L->inv_o));
+  int k = L->kind;
+  if (k == RT_N_SPHERE) {                                                  // math_shapes.rs:42-62
+    V3 v = sub(o, ld3(L->c));
+    double il = 1.0 / len(d);
+    V3 dn = scale(d, il);
+    double vd = dot(v, dn);
+    double sum = vd * vd - (dot(v, v) - L->r2);
+    if (sum < 0.0) return 0;
+    double sq = sqrt(sum);
+    *t0 = (-vd + sq) * il;
+    *t1 = (-vd - sq) * il;
+    return 2;
+  }
+  if (k == RT_N_PLANE) {                                                   // :168-180
+    V3 pn = ld3(L->pnorm);
+    double v_d = dot(pn, d);
+    if (v_d != 0.0) {
+      double t = -(dot(pn, o) + L->pl[0][3]) * (1.0 / v_d);
+      if (t >= 0.0) { *t0 = t; return 1; }
+    }
+    return 0;
+  }
+  double tn = -INFINITY, tf = INFINITY;                                    // :248-290
+#define RT_SLAB(P, D, I)                                                    \
+  if (D == 0.0) {                                                           \
+    if (P < L->lo[I] || P > L->hi[I]) return 0;                             \
+  } else {                                                                  \
+    double a = (L->lo[I] - P) / D, b = (L->hi[I] - P) / D;                  \
+    if (a > b) { double tmp = a; a = b; b = tmp; }                          \
+    if (a > tn) tn = a;                                                     \
+    if (b < tf) tf = b;                                                     \
+    if (tn > tf || tf < 0.0) return 0;                                      \
+  }
+  RT_SLAB(o.x, d.x, 0)
+  RT_SLAB(o.y, d.y, 1)
+  RT_SLAB(o.z, d.z, 2)
+#undef RT_SLAB
+  *t0 = tn;
+  *t1 = tf;
+  return 2;
+}
+
+// Conjunction of every CSG ancestor's sibling test for a hit of leaf L at world point p
+// (csg.rs:43-95), as a postfix program over a bit stack.
+__device__ bool leaf_filter(const RtDevScene& S, const RtLeaf* L, V3 p) {
+  uint32_t st = 0;
+  const int e = L->prog_end;
+  for (int k = L->prog_begin; k < e; ++k) {
+    const RtProg pr = S.prog[k];
+    if (pr.op == RT_OP_INSIDE) {
+      st = (st << 1) | (leaf_inside(&S.leaves[pr.arg], p) ? 1u : 0u);
+    } else if (pr.op == RT_OP_REQUIRE) {
+      uint32_t v = st & 1u;
+      st >>= 1;
+      if (v != (uint32_t)pr.arg) return false;
+    } else {
+      uint32_t b = st & 1u;
+      st >>= 1;
+      uint32_t a = st & 1u, r;
+      if (pr.op == RT_OP_AND) r = a & b;
+      else if (pr.op == RT_OP_OR) r = a | b;
+      else r = a & (b ^ 1u);
+      st = (st & ~1u) | r;
+    }
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ traversal (raytracer.rs)
+// Nearest hit over all objects in draw order: accept d if d > EPS && d < nearest
+// (raytracer.rs:141-150).  The acceptance test is pure, so it runs BEFORE the (pure) CSG
+// filter: candidates that cannot win never pay for the sibling is_inside tests.
+__device__ int nearest_hit(const RtDevScene& S, V3 ro, V3 rd, double* dist) {
+  double best = INFINITY;
+  int bobj = -1;
+  for (int o = 0; o < S.n_objects; ++o) {
+    const RtObject* O = &S.objects[o];
+    const int lb = O->leaf_begin, le = lb + O->leaf_count;
+    for (int l = lb; l < le; ++l) {
+      const RtLeaf* L = &S.leaves[l];
+      double t0 = 0.0, t1 = 0.0;
+      int n = leaf_candidates(L, ro, rd, &t0, &t1);
+      const bool filtered = L->prog_end != L->prog_begin;
+      if (n >= 1 && t0 > EPS && t0 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) {
+        best = t0; bobj = o;
+      }
+      if (n >= 2 && t1 > EPS && t1 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t1))))) {
+        best = t1; bobj = o;
+      }
+    }
+  }
+  *dist = best;
+  return bobj;
+}
+
+// Product of the transparencies of every filtered hit with EPS < d < dist (raytracer.rs:181-197).
+// Early-out once the product is exactly 0 (it stays 0: every factor is finite, checked on the
+// host), objects of transparency exactly 1.0 are skipped (x * 1.0 == x).
+__device__ double shadow_transparency(const RtDevScene& S, V3 p, V3 dir, double dist) {
+  double tr = 1.0;
+  for (int o = 0; o < S.n_objects; ++o) {
+    const RtObject* O = &S.objects[o];
+    if (O->shadow_skip) continue;
+    const double tobj = O->transparency;
+    const int lb = O->leaf_begin, le = lb + O->leaf_count;
+    for (int l = lb; l < le; ++l) {
+      const RtLeaf* L = &S.leaves[l];
+      double t0 = 0.0, t1 = 0.0;
+      int n = leaf_candidates(L, p, dir, &t0, &t1);
+      const bool filtered = L->prog_end != L->prog_begin;
+      if (n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) {
+        tr *= tobj;
+        if (tr == 0.0 && S.shadow_early_out) return 0.0;
+      }
+      if (n >= 2 && t1 > EPS && t1 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t1))))) {
+        tr *= tobj;
+        if (tr == 0.0 && S.shadow_early_out) return 0.0;
+      }
+    }
+  }
+  return tr;
+}
+
+// Normal and UV of top-level object O at point p: RTObject shape get_normal / get_uv_coordinates,
+// with CSG's is_on_surface / is_inside evaluated bottom-up over the post-order node list
+// (csg.rs:98-168) and the descent a-then-b of csg.rs:104-121 / :161-167.
+__device__ void object_normal_uv(const RtDevScene& S, const RtObject* O, V3 p, bool want_uv, V3* n,
+                                 double* u, double* v) {
+  const RtNode* N = S.nodes + O->node_begin;
+  const int cnt = O->node_count;
+  *u = 0.0;
+  *v = 0.0;
+  if (cnt == 1) {
+    const RtLeaf* L = &S.leaves[N[0].leaf];
+    *n = leaf_normal(L, p);
+    if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
+    return;
+  }
+  uint32_t in = 0, on = 0;
+  for (int i = 0; i < cnt; ++i) {
+    const RtNode nd = N[i];
+    bool bi, bo;
+    if (nd.kind < RT_N_UNION) {
+      const RtLeaf* L = &S.leaves[nd.leaf];
+      bi = leaf_inside(L, p);
+      bo = leaf_on_surface(L, p);
+    } else {
+      bool ia = (in >> nd.a) & 1u, ib = (in >> nd.b) & 1u, oa = (on >> nd.a) & 1u, ob = (on >> nd.b) & 1u;
+      if (nd.kind == RT_N_UNION) { bi = ia || ib; bo = (oa && !ib) || (ob && !ia); }
+      else if (nd.kind == RT_N_INTERSECTION) { bi = ia && ib; bo = (oa && ib) || (ob && ia); }
+      else { bi = ia && !ib; bo = (oa && !ib) || (ob && ia); }
+    }
+    in |= (uint32_t)bi << i;
+    on |= (uint32_t)bo << i;
+  }
+  int cur = cnt - 1;
+  bool neg = false;
+  for (;;) {
+    const RtNode nd = N[cur];
+    if (nd.kind < RT_N_UNION) {
+      const RtLeaf* L = &S.leaves[nd.leaf];
+      *n = leaf_normal(L, p);
+      if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
+      break;
+    }
+    if ((on >> nd.a) & 1u) {
+      cur = nd.a;
+    } else if ((on >> nd.b) & 1u) {
+      if (nd.kind == RT_N_DIFFERENCE) neg = !neg;           // b.get_normal(p) * -1.0
+      cur = nd.b;
+    } else {
+      *n = {1.0, 0.0, 0.0};                                 // fallback; UV is Err -> (0,0)
+      break;
+    }
+  }
+  if (neg) *n = scale(*n, -1.0);
+}
+
+// PixmapTexture::get_color_at (texture.rs:27-34) on RGBA8 texels, /255.0 (sceneparser/texture.rs:29-33)
+__device__ Col texture_color(const RtDevScene& S, int tex, double u, double v) {
+  const RtTexture T = S.textures[tex];
+  double x = u * (double)(T.w - 1);
+  double y = (double)T.h - (v * (double)(T.h - 1)) - 1.0;
+  // `as usize` saturates (NaN/negative -> 0); the reference would panic past the edge: clamp.
+  int xi = x > 0.0 ? (x < (double)(T.w - 1) ? (int)x : T.w - 1) : 0;
+  int yi = y > 0.0 ? (y < (double)(T.h - 1) ? (int)y : T.h - 1) : 0;
+  const uint32_t px = *(const uint32_t*)(S.texels + T.offset + ((size_t)yi * T.w + xi) * 4);
+  return {(double)(px & 0xffu) / 255.0, (double)((px >> 8) & 0xffu) / 255.0, (double)((px >> 16) & 0xffu) / 255.0};
+}
+
+__device__ __forceinline__ V3 reflect_dir(V3 i, V3 n) {                    // raytracer.rs:332-334
+  return sub(i, scale(scale(n, 2.0), dot(n, i)));
+}
+__device__ __forceinline__ V3 refract_dir(V3 i, V3 n, double r, bool* tir) {   // raytracer.rs:336-353
+  double cos_1 = dot(scale(i, -1.0), n);
+  double v = 1.0 - r * r * (1.0 - cos_1 * cos_1);
+  *tir = v < 0.0;
+  if (*tir) return {0.0, 0.0, 0.0};
+  double cos_2 = sqrt(v);
+  return normalized(add(scale(i, r), scale(n, r * cos_1 - cos_2)));
+}
+
+// get_ray_color (raytracer.rs:132-287) for one primary ray, recursion unrolled onto a per-lane
+// frame stack.  REFR = the scene has a transparent object (refraction frames need more state).
+template <bool REFR>
+__device__ Col trace(const RtDevScene& S, V3 ro, V3 rd, int max_depth) {
+  double fA[RT_MAX_DEPTH_CAP][3];     // parent colour already intensified by (1 - w)
+  double fW[RT_MAX_DEPTH_CAP];        // child weight w (transparency or reflectivity)
+  double fP[REFR ? RT_MAX_DEPTH_CAP : 1][3], fD[REFR ? RT_MAX_DEPTH_CAP : 1][3];
+  double fRP[REFR ? RT_MAX_DEPTH_CAP : 1];
+  int fPend[REFR ? RT_MAX_DEPTH_CAP : 1];
+  int sp = 0, depth = 0;
+  Col C = {0.0, 0.0, 0.0};
+  for (;;) {
+    bool descend = false;
+    double t_hit;
+    const int oi = nearest_hit(S, ro, rd, &t_hit);
+    if (oi < 0) {
+      C = {0.0, 0.0, 0.0};                                               // Color::BLACK (:152-160)
+    } else {
+      const RtObject* O = &S.objects[oi];
+      const V3 p = add(ro, scale(rd, t_hit));                             // :162
+      V3 nrm;
+      double u, v;
+      object_normal_uv(S, O, p, O->textured != 0, &nrm, &u, &v);
+      nrm = normalized(nrm);                                              // :163
+      Col c = O->textured ? texture_color(S, O->tex, u, v) : Col{O->color[0], O->color[1], O->color[2]};
+      Col L = cmul(c, in_range(0.6, 0.6, 0.6));                           // ambient (:172)
+      for (int li = 0; li < S.n_lights; ++li) {                           // :175-228
+        const RtLight lt = S.lights[li];
+        const V3 lp = ld3(lt.p);
+        const V3 lv = sub(lp, p);
+        const V3 sdir = normalized(lv);
+        const double dist = len(lv);
+        const double tr = shadow_transparency(S, p, sdir, dist);
+        if (tr == 0.0) continue;
+        double ang = acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
+        if (ang >= PI_D / 2.0) ang = PI_D - ang;
+        const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
+        const Col lc = intensify(intensify(Col{lt.col[0], lt.col[1], lt.col[2]}, inten), tr);
+        L = cadd(L, cmul(c, lc));
+      }
+      const V3 nd = scale(rd, -1.0);                                      // :230-235
+      const bool inside = acos(dot(nd, nrm) / (len(nd) * len(nrm))) >= PI_D / 2.0;
+      const V3 n2 = inside ? scale(nrm, -1.0) : nrm;
+      const double r1 = inside ? 1.45 : 1.0, r2 = inside ? 1.0 : 1.45;
+      const double transp = O->transparency, refl = O->reflectivity;
+      bool tir = false;
+      V3 tdir = {0.0, 0.0, 0.0};
+      const bool do_refr = REFR && depth < max_depth && transp != 0.0;   // :242
+      if (do_refr) tdir = refract_dir(rd, n2, r1 / r2, &tir);
+      const double rp = tir ? refl + (1.0 - refl) * transp : refl;       // :261-265
+      const bool do_refl = depth < max_depth && rp != 0.0 && (!inside || tir);   // :267
+      if (do_refr && !tir) {
+        Col A = intensify(L, 1.0 - transp);
+        fA[sp][0] = A.r; fA[sp][1] = A.g; fA[sp][2] = A.b;
+        fW[sp] = transp;
+        if constexpr (REFR) {
+          fPend[sp] = do_refl ? 1 : 0;
+          if (do_refl) {
+            V3 rdir = reflect_dir(rd, n2);
+            fP[sp][0] = p.x; fP[sp][1] = p.y; fP[sp][2] = p.z;
+            fD[sp][0] = rdir.x; fD[sp][1] = rdir.y; fD[sp][2] = rdir.z;
+            fRP[sp] = rp;
+          }
+        }
+        ++sp;
+        ro = p;
+        rd = tdir;
+        depth = sp;
+        descend = true;
+      } else if (do_refl) {
+        Col A = intensify(L, 1.0 - rp);
+        fA[sp][0] = A.r; fA[sp][1] = A.g; fA[sp][2] = A.b;
+        fW[sp] = rp;
+        if constexpr (REFR) fPend[sp] = 0;
+        ++sp;
+        rd = reflect_dir(rd, n2);
+        ro = p;
+        depth = sp;
+        descend = true;
+      } else {
+        C = L;
+      }
+    }
+    if (descend) continue;
+    while (sp > 0) {                                                      // post-order combine
+      const int f = sp - 1;
+      const Col comb = cadd(Col{fA[f][0], fA[f][1], fA[f][2]}, intensify(C, fW[f]));
+      if constexpr (REFR) {
+        if (fPend[f]) {                                                   // refraction done -> reflection
+          fPend[f] = 0;
+          Col A = intensify(comb, 1.0 - fRP[f]);
+          fA[f][0] = A.r; fA[f][1] = A.g; fA[f][2] = A.b;
+          fW[f] = fRP[f];
+          ro = {fP[f][0], fP[f][1], fP[f][2]};
+          rd = {fD[f][0], fD[f][1], fD[f][2]};
+          depth = sp;
+          descend = true;
+          break;
+        }
+      }
+      C = comb;
+      --sp;
+    }
+    if (!descend) return C;
+  }
+}
+
+// PerspectiveCamera::create_ray (camera.rs:65-74)
+__device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double y, V3* ro, V3* rd) {
+  double sx = ((x / cam.width) - 0.5) * cam.aspect;
+  double sy = (cam.height - 1.0 - y) / cam.height - 0.5;
+  *rd = add(add(ld3(cam.direction), scale(ld3(cam.right), sx)), scale(ld3(cam.up), sy));
+  *ro = ld3(cam.center);
+}
+
+// Rows [y0, y1) of the full frame.  Workgroup = 16x16 pixels, wave = 8x8.
+template <bool REFR, bool F64>
+__global__ __launch_bounds__(256) void render_rows_kernel(RtDevScene S, int y0, int y1, int max_depth,
+                                                          uint8_t* __restrict__ out, size_t stride) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tiles_x = (S.width + 15) >> 4;
+  const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
+  const int x = (bx << 4) + ((wave & 1) << 3) + (lane & 7);
+  const int y = y0 + (by << 4) + ((wave >> 1) << 3) + (lane >> 3);
+  if (x >= S.width || y >= y1) return;
+  V3 ro, rd;
+  camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
+  const Col c = trace<REFR>(S, ro, rd, max_depth);
+  uint8_t* row = out + (size_t)(y - y0) * stride;
+  if constexpr (F64) {
+    double* o = (double*)row + (size_t)x * 4;
+    o[0] = c.r; o[1] = c.g; o[2] = c.b; o[3] = 1.0;                        // alpha is 1 after any colour op
+  } else {
+    ((uint32_t*)row)[x] = to_u8(c.r) | (to_u8(c.g) << 8) | (to_u8(c.b) << 16) | (255u << 24);
+  }
+}
+
+template <bool REFR>
+__global__ __launch_bounds__(256) void render_points_kernel(RtDevScene S, const double* __restrict__ xy,
+                                                            size_t n, int max_depth, double* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  V3 ro, rd;
+  camera_ray(S.cam, xy[2 * i], xy[2 * i + 1], &ro, &rd);
+  const Col c = trace<REFR>(S, ro, rd, max_depth);
+  out[4 * i] = c.r; out[4 * i + 1] = c.g; out[4 * i + 2] = c.b; out[4 * i + 3] = 1.0;
+}
+
+}  // namespace
+
+// ====================================================================== device context
+struct rt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  void* d_blob = nullptr;
+  size_t blob_bytes = 0;
+  RtDevScene dev;
+  int32_t max_depth = 10;
+  bool uploaded = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+};
+
+using rt::fail;
+
+#define RT_HIP(call)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) return fail(RT_ERR_DEVICE, "%s failed: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+static int ensure_scratch(rt_ctx* c, size_t bytes) {
+  if (c->scratch_bytes >= bytes) return RT_OK;
+  if (c->scratch) (void)hipFree(c->scratch);
+  c->scratch = nullptr;
+  c->scratch_bytes = 0;
+  RT_HIP(hipMalloc(&c->scratch, bytes));
+  c->scratch_bytes = bytes;
+  return RT_OK;
+}
+
+static bool is_device_ptr(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+template <typename T>
+static size_t put(std::vector<uint8_t>& blob, const std::vector<T>& v) {
+  size_t off = (blob.size() + 255) & ~(size_t)255;
+  blob.resize(off + v.size() * sizeof(T) + 16);
+  if (!v.empty()) memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+  return off;
+}
+
+extern "C" {
+
+int rt_device_count(int* count) {
+  if (!count) return fail(RT_ERR_INVALID, "null output");
+  *count = 0;
+  hipError_t e = hipGetDeviceCount(count);
+  if (e != hipSuccess) { *count = 0; return fail(RT_ERR_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e)); }
+  return RT_OK;
+}
+
+int rt_ctx_create(int device, rt_ctx** out) {
+  if (!out) return fail(RT_ERR_INVALID, "null output");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RT_ERR_DEVICE, "no HIP device available");
+  if (device < 0 || device >= n) return fail(RT_ERR_INVALID, "device %d out of range (%d devices)", device, n);
+  RT_HIP(hipSetDevice(device));
+  rt_ctx* c = new rt_ctx();
+  c->device = device;
+  memset(&c->dev, 0, sizeof c->dev);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    delete c;
+    return fail(RT_ERR_DEVICE, "stream/event creation failed");
+  }
+  *out = c;
+  return RT_OK;
+}
+
+int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
+  if (!c || !s) return fail(RT_ERR_INVALID, "null argument");
+  rt::FlatScene f;
+  int rc = rt::flatten(*s, &f);
+  if (rc) return rc;
+  std::vector<uint8_t> blob;
+  size_t o_obj = put(blob, f.objects), o_nodes = put(blob, f.nodes), o_leaves = put(blob, f.leaves);
+  size_t o_prog = put(blob, f.prog), o_lights = put(blob, f.lights), o_tex = put(blob, f.textures);
+  size_t o_texels = put(blob, f.texels);
+  RT_HIP(hipSetDevice(c->device));
+  if (c->d_blob) { (void)hipFree(c->d_blob); c->d_blob = nullptr; }
+  c->uploaded = false;
+  RT_HIP(hipMalloc(&c->d_blob, blob.size()));
+  RT_HIP(hipMemcpy(c->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
+  c->blob_bytes = blob.size();
+  uint8_t* b = (uint8_t*)c->d_blob;
+  RtDevScene& d = c->dev;
+  d.objects = (const RtObject*)(b + o_obj);
+  d.nodes = (const RtNode*)(b + o_nodes);
+  d.leaves = (const RtLeaf*)(b + o_leaves);
+  d.prog = (const RtProg*)(b + o_prog);
+  d.lights = (const RtLight*)(b + o_lights);
+  d.textures = (const RtTexture*)(b + o_tex);
+  d.texels = b + o_texels;
+  d.n_objects = (int32_t)f.objects.size();
+  d.n_lights = (int32_t)f.lights.size();
+  d.n_leaves = (int32_t)f.leaves.size();
+  d.n_nodes = (int32_t)f.nodes.size();
+  d.width = f.width;
+  d.height = f.height;
+  d.any_transparent = f.any_transparent;
+  d.shadow_early_out = f.shadow_early_out;
+  d.cam = f.cam;
+  c->max_depth = f.max_depth;
+  c->uploaded = true;
+  return RT_OK;
+}
+
+static int launch_rows(rt_ctx* c, uint32_t y0, uint32_t y1, int32_t max_depth, void* out, size_t stride,
+                       void* stream, bool f64) {
+  if (!c || !out) return fail(RT_ERR_INVALID, "null argument");
+  if (!c->uploaded) return fail(RT_ERR_INVALID, "no scene uploaded to this context");
+  if (y0 > y1 || y1 > (uint32_t)c->dev.height) return fail(RT_ERR_INVALID, "bad row range [%u, %u) for height %d", y0, y1, c->dev.height);
+  size_t row_bytes = (size_t)c->dev.width * (f64 ? 32 : 4);
+  if (stride < row_bytes) return fail(RT_ERR_INVALID, "row stride %zu < %zu", stride, row_bytes);
+  if (max_depth < 0) max_depth = c->max_depth;
+  if (max_depth > RT_MAX_DEPTH_CAP) return fail(RT_ERR_UNSUPPORTED, "max_depth %d > %d", max_depth, RT_MAX_DEPTH_CAP);
+  if (y0 == y1) return RT_OK;
+  RT_HIP(hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  const bool dev_out = is_device_ptr(out);
+  uint8_t* target = (uint8_t*)out;
+  size_t tstride = stride;
+  if (!dev_out) {
+    int rc = ensure_scratch(c, row_bytes * (y1 - y0));
+    if (rc) return rc;
+    target = (uint8_t*)c->scratch;
+    tstride = row_bytes;
+  }
+  const int tiles_x = (c->dev.width + 15) / 16, tiles_y = (int)((y1 - y0 + 15) / 16);
+  dim3 grid((unsigned)(tiles_x * tiles_y)), block(256);
+  RT_HIP(hipEventRecord(c->ev0, st));
+  const bool refr = c->dev.any_transparent != 0;
+  if (refr && f64) hipLaunchKernelGGL((render_rows_kernel<true, true>), grid, block, 0, st, c->dev, (int)y0, (int)y1, max_depth, target, tstride);
+  else if (refr) hipLaunchKernelGGL((render_rows_kernel<true, false>), grid, block, 0, st, c->dev, (int)y0, (int)y1, max_depth, target, tstride);
+  else if (f64) hipLaunchKernelGGL((render_rows_kernel<false, true>), grid, block, 0, st, c->dev, (int)y0, (int)y1, max_depth, target, tstride);
+  else hipLaunchKernelGGL((render_rows_kernel<false, false>), grid, block, 0, st, c->dev, (int)y0, (int)y1, max_depth, target, tstride);
+  RT_HIP(hipGetLastError());
+  RT_HIP(hipEventRecord(c->ev1, st));
+  c->timed = true;
+  if (!dev_out) {
+    RT_HIP(hipMemcpy2DAsync(out, stride, target, tstride, row_bytes, y1 - y0, hipMemcpyDeviceToHost, st));
+    RT_HIP(hipStreamSynchronize(st));
+  }
+  return RT_OK;
+}
+
+int rt_render_rows(rt_ctx* c, uint32_t y0, uint32_t y1, int32_t max_depth, uint8_t* rgba8,
+                   size_t row_stride_bytes, void* stream) {
+  return launch_rows(c, y0, y1, max_depth, rgba8, row_stride_bytes, stream, false);
+}
+
+int rt_render_rows_f64(rt_ctx* c, uint32_t y0, uint32_t y1, int32_t max_depth, double* rgba,
+                       size_t row_stride_bytes, void* stream) {
+  return launch_rows(c, y0, y1, max_depth, rgba, row_stride_bytes, stream, true);
+}
+
+int rt_render_points_f64(rt_ctx* c, const double* xy, size_t n, int32_t max_depth, double* out, void* stream) {
+  if (!c || !xy || !out) return fail(RT_ERR_INVALID, "null argument");
+  if (!c->uploaded) return fail(RT_ERR_INVALID, "no scene uploaded to this context");
+  if (max_depth < 0) max_depth = c->max_depth;
+  if (max_depth > RT_MAX_DEPTH_CAP) return fail(RT_ERR_UNSUPPORTED, "max_depth %d > %d", max_depth, RT_MAX_DEPTH_CAP);
+  if (n == 0) return RT_OK;
+  RT_HIP(hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  const bool dev_in = is_device_ptr(xy), dev_out = is_device_ptr(out);
+  const double* in = xy;
+  double* target = out;
+  if (!dev_in || !dev_out) {
+    int rc = ensure_scratch(c, n * 6 * sizeof(double));
+    if (rc) return rc;
+    double* sx = (double*)c->scratch;
+    if (!dev_in) { RT_HIP(hipMemcpyAsync(sx, xy, n * 2 * sizeof(double), hipMemcpyHostToDevice, st)); in = sx; }
+    if (!dev_out) target = sx + 2 * n;
+  }
+  dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  RT_HIP(hipEventRecord(c->ev0, st));
+  if (c->dev.any_transparent) hipLaunchKernelGGL((render_points_kernel<true>), grid, block, 0, st, c->dev, in, n, max_depth, target);
+  else hipLaunchKernelGGL((render_points_kernel<false>), grid, block, 0, st, c->dev, in, n, max_depth, target);
+  RT_HIP(hipGetLastError());
+  RT_HIP(hipEventRecord(c->ev1, st));
+  c->timed = true;
+  if (!dev_out) {
+    RT_HIP(hipMemcpyAsync(out, target, n * 4 * sizeof(double), hipMemcpyDeviceToHost, st));
+    RT_HIP(hipStreamSynchronize(st));
+  }
+  return RT_OK;
+}
+
+int rt_ctx_last_kernel_ms(rt_ctx* c, float* ms) {
+  if (!c || !ms) return fail(RT_ERR_INVALID, "null argument");
+  if (!c->timed) return fail(RT_ERR_INVALID, "no launch recorded");
+  RT_HIP(hipEventSynchronize(c->ev1));
+  RT_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return RT_OK;
+}
+
+int rt_ctx_synchronize(rt_ctx* c) {
+  if (!c) return fail(RT_ERR_INVALID, "null context");
+  RT_HIP(hipSetDevice(c->device));
+  RT_HIP(hipStreamSynchronize(c->stream));
+  return RT_OK;
+}
+
+void rt_ctx_free(rt_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->d_blob) (void)hipFree(c->d_blob);
+  if (c->scratch) (void)hipFree(c->scratch);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+}  // extern "C"

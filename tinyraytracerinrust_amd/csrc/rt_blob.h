@@ -1,0 +1,106 @@
+// rt_blob.h -- the flattened, immutable scene as it lives in HBM (shared by the host
+// flattener, scene_flatten.cpp, and the gfx950 kernels, render_kernels.hip).
+//
+// Design (DESIGN.md "Data layout in HBM"):
+//  * The reference walks a tree of boxed trait objects per ray (RTObject -> dyn MathShape
+//    -> CSG -> RTObject ...).  Here every top-level object is flattened once on the host into
+//      - a contiguous run of RtNode in POST-ORDER (children before parents, root last), used
+//        to evaluate CSG is_inside / is_on_surface bottom-up at a shaded point;
+//      - a contiguous run of RtLeaf (the primitives, DFS order), each carrying everything the
+//        reference recomputes per call (inverse-origin, normalised plane normal, r*r, r+EPS,
+//        cube slab bounds, the six cube "quirk" planes and their transformed normals), computed
+//        on the host with the IDENTICAL f64 op sequence so the device reads bit-equal values;
+//      - per leaf, a tiny postfix "hit filter" program: the conjunction of the sibling
+//        is_inside tests every CSG ancestor applies to a hit of that leaf (csg.rs:39-96).
+//  * All indices into these arrays are wave-uniform in the kernels (every lane walks the same
+//    object list), so the loads compile to scalar (SMEM) loads through the scalar cache.
+//  * Textures stay RGBA8 in HBM (the reference holds f64 RGBA, 32 B/texel); the kernel
+//    converts with /255.0 exactly as sceneparser/texture.rs:29-33 does.
+#pragma once
+#include <stdint.h>
+
+#define RT_EPSILON 10e-7            /* math.rs:2 */
+#define RT_MAX_DEPTH_CAP 16          /* recursion frames kept per lane (max_depth <= 16) */
+
+enum RtNodeKind : int32_t {
+  RT_N_SPHERE = 0, RT_N_PLANE = 1, RT_N_CUBE = 2,
+  RT_N_UNION = 3, RT_N_INTERSECTION = 4, RT_N_DIFFERENCE = 5
+};
+
+// Hit-filter program opcodes (postfix over a bit stack).
+enum RtProgOp : int32_t {
+  RT_OP_INSIDE = 0,     // push leaf[arg].is_inside(p)
+  RT_OP_AND = 1,        // a && b
+  RT_OP_OR = 2,         // a || b
+  RT_OP_ANDNOT = 3,     // a && !b
+  RT_OP_REQUIRE = 4,    // pop v; filter &= (v == arg)
+};
+
+struct RtProg { int32_t op, arg; };
+
+struct alignas(16) RtLeaf {
+  double inv[12];       // inverse matrix rows 0..2 (row-major, 4 per row)
+  double inv_o[3];      // transform_vector((0,0,0), inverse)   (transformation.rs:80-83)
+  double mat[12];       // forward matrix rows 0..2
+  double mat_o[3];      // transform_vector((0,0,0), matrix)    (transformation.rs:71-74)
+  double c[3];          // sphere / cube centre
+  double radius;        // sphere radius | cube half length ("length", math_shapes.rs:229)
+  double r2;            // sphere: radius * radius
+  double r_eps;         // sphere: radius + EPSILON
+  double lo[3];         // cube: centre - length
+  double hi[3];         // cube: centre + length
+  double lo_e[3];       // cube: centre - length - EPSILON
+  double hi_e[3];       // cube: centre + length + EPSILON
+  double pl[6][4];      // plane leaf: pl[0] = raw (a,b,c,d); cube: p1..p6 raw (a,b,c,d)
+  double pn[6][3];      // matching transformed unit normals (MathPlane::normal)
+  double pnorm[3];      // plane leaf: Vector::new(a,b,c).normalized() (math_shapes.rs:169)
+  int32_t kind;         // RtNodeKind (leaf kinds only)
+  int32_t prog_begin;   // hit-filter program [prog_begin, prog_end)
+  int32_t prog_end;
+  int32_t pad;
+};
+
+struct RtNode {
+  int32_t kind;         // RtNodeKind
+  int32_t a, b;         // CSG children: node indices relative to the object's node_begin
+  int32_t leaf;         // leaf kinds: global leaf index
+};
+
+struct alignas(16) RtObject {
+  int32_t node_begin, node_count;   // post-order; root = node_begin + node_count - 1
+  int32_t leaf_begin, leaf_count;
+  int32_t textured;                 // 0 solid, 1 texture
+  int32_t tex;                      // texture index
+  int32_t shadow_skip;              // transparency == 1.0: shadow multiplies by 1 -> no-op
+  int32_t pad;
+  double color[3];                  // material colour (solid)
+  double reflectivity, transparency;
+};
+
+struct RtTexture {
+  int64_t offset;                   // byte offset of RGBA8 data in the texel pool
+  int32_t w, h;
+};
+
+struct RtLight { double p[3]; double col[3]; };
+
+struct RtCamera {
+  double center[3], direction[3], right[3], up[3];
+  double aspect, width, height;     // as f64: `self.width as f64` (camera.rs:67-68)
+};
+
+// Kernel argument block (passed by value; all pointers are device pointers).
+struct RtDevScene {
+  const RtObject* objects;
+  const RtNode* nodes;
+  const RtLeaf* leaves;
+  const RtProg* prog;
+  const RtLight* lights;
+  const RtTexture* textures;
+  const uint8_t* texels;
+  int32_t n_objects, n_lights, n_leaves, n_nodes;
+  int32_t width, height;
+  int32_t any_transparent;          // some object has transparency != 0 (refraction possible)
+  int32_t shadow_early_out;         // every transparency is finite: product==0 stays 0
+  RtCamera cam;
+};

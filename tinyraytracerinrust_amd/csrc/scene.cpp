@@ -1,0 +1,500 @@
+// scene.cpp -- scene-construction half of the C ABI (rt_xform_*, rt_scene_*, rt_shape_*)
+// and the host flattener that turns the RayTracer-shaped rt_scene into the HBM layout of
+// rt_blob.h.  Compiled with -ffp-contract=off: every precomputed value is produced with the
+// same f64 op sequence the reference evaluates per call, so the device reads bit-equal data.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <new>
+#include <string>
+#include <vector>
+
+#include "scene.h"
+
+namespace rt {
+
+static thread_local std::string g_last_error;
+
+void set_error_message(const std::string& msg) { g_last_error = msg; }
+
+int fail(int status, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return status;
+}
+
+// ---------------------------------------------------------------- transformations
+// transformation.rs:208-220 -- accumulate from 0.0 in k order.
+static void mat_mul(const double* a, const double* b, double* out) {
+  double r[16];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) {
+      double acc = 0.0;
+      for (int k = 0; k < 4; ++k) acc += a[4 * i + k] * b[4 * k + j];
+      r[4 * i + j] = acc;
+    }
+  memcpy(out, r, sizeof r);
+}
+
+static void set_identity(double* m) {
+  memset(m, 0, 16 * sizeof(double));
+  m[0] = m[5] = m[10] = m[15] = 1.0;
+}
+
+void xf_identity(rt_transformation* t) {                       // :104-113
+  set_identity(t->matrix);
+  set_identity(t->inverse);
+}
+
+void xf_translation(double x, double y, double z, rt_transformation* t) {   // :164-180
+  xf_identity(t);
+  t->matrix[3] = x; t->matrix[7] = y; t->matrix[11] = z;
+  t->inverse[3] = -x; t->inverse[7] = -y; t->inverse[11] = -z;
+}
+
+void xf_scaling(double x, double y, double z, rt_transformation* t) {      // :182-198
+  xf_identity(t);
+  t->matrix[0] = x; t->matrix[5] = y; t->matrix[10] = z;
+  t->inverse[0] = 1.0 / x; t->inverse[5] = 1.0 / y; t->inverse[10] = 1.0 / z;
+}
+
+// Elementary rotations (:116-147); `axis` 0/1/2.
+static void rotation_about(int axis, double angle, double* m) {
+  double c = cos(angle), s = sin(angle);
+  set_identity(m);
+  if (axis == 0) { m[5] = c; m[6] = -s; m[9] = s; m[10] = c; }
+  else if (axis == 1) { m[0] = c; m[2] = -s; m[8] = s; m[10] = c; }
+  else { m[0] = c; m[1] = -s; m[4] = s; m[5] = c; }
+}
+
+void xf_rotation(double x, double y, double z, rt_transformation* t) {     // :115-162
+  double m1[16], m2[16], m3[16], i1[16], i2[16], i3[16], tmp[16];
+  rotation_about(0, x, m1); rotation_about(0, -x, i1);
+  rotation_about(1, y, m2); rotation_about(1, -y, i2);
+  rotation_about(2, z, m3); rotation_about(2, -z, i3);
+  mat_mul(m1, m2, tmp); mat_mul(tmp, m3, t->matrix);
+  mat_mul(i1, i2, tmp); mat_mul(tmp, i3, t->inverse);   // Rx(-x)Ry(-y)Rz(-z): the reference's "inverse"
+}
+
+void xf_compose(const rt_transformation& self, const rt_transformation& other, rt_transformation* out) {
+  rt_transformation r;                                     // :200-205
+  mat_mul(other.matrix, self.matrix, r.matrix);
+  mat_mul(self.inverse, other.inverse, r.inverse);
+  *out = r;
+}
+
+// transform_vector (:53-59): ((m0*x + m1*y) + m2*z) + m3 per row.
+void xf_apply(const double m[16], const double v[3], double out[3]) {
+  double a = m[0] * v[0] + m[1] * v[1] + m[2] * v[2] + m[3];
+  double b = m[4] * v[0] + m[5] * v[1] + m[6] * v[2] + m[7];
+  double c = m[8] * v[0] + m[9] * v[1] + m[10] * v[2] + m[11];
+  out[0] = a; out[1] = b; out[2] = c;
+}
+
+// ---------------------------------------------------------------- small f64 vector helpers
+struct V { double x, y, z; };
+static inline double dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }         // vector.rs:94-100
+static inline V scale(V a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+static inline V sub(V a, V b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static inline double length(V a) { return sqrt(dot(a, a)); }
+static inline V normalized(V a) { return scale(a, 1.0 / length(a)); }                   // vector.rs:45-47
+static inline V cross(V a, V b) {                                                        // vector.rs:61-67
+  return {a.y * b.z - a.z * b.y, a.x * b.z - a.z * b.x, a.x * b.y - a.y * b.x};
+}
+static inline V apply(const double m[16], V v) {
+  double in[3] = {v.x, v.y, v.z}, o[3];
+  xf_apply(m, in, o);
+  return {o[0], o[1], o[2]};
+}
+// transform_direction_vector (:70-77): T(v) - T(0)
+static inline V apply_dir(const double m[16], V v) { return sub(apply(m, v), apply(m, {0.0, 0.0, 0.0})); }
+
+// ---------------------------------------------------------------- flattening
+static void leaf_common(const rt_transformation& t, RtLeaf* L) {
+  memset(L, 0, sizeof *L);
+  memcpy(L->inv, t.inverse, 12 * sizeof(double));
+  memcpy(L->mat, t.matrix, 12 * sizeof(double));
+  V io = apply(t.inverse, {0.0, 0.0, 0.0});
+  V mo = apply(t.matrix, {0.0, 0.0, 0.0});
+  L->inv_o[0] = io.x; L->inv_o[1] = io.y; L->inv_o[2] = io.z;
+  L->mat_o[0] = mo.x; L->mat_o[1] = mo.y; L->mat_o[2] = mo.z;
+}
+
+// MathPlane::new (math_shapes.rs:140-152): raw (a,b,c,d) + transformed unit normal.
+static void plane_into(const rt_transformation& t, double a, double b, double c, double d,
+                       double pl[4], double pn[3]) {
+  pl[0] = a; pl[1] = b; pl[2] = c; pl[3] = d;
+  V n = normalized({a, b, c});
+  V tn = normalized(apply_dir(t.matrix, n));                  // transformed_normal (:158-160)
+  pn[0] = tn.x; pn[1] = tn.y; pn[2] = tn.z;
+}
+
+static int make_leaf(const ShapeRec& s, RtLeaf* L) {
+  leaf_common(s.t, L);
+  const double EPS = RT_EPSILON;
+  switch (s.kind) {
+    case SHAPE_SPHERE: {                                        // math_shapes.rs:28-39
+      L->kind = RT_N_SPHERE;
+      for (int i = 0; i < 3; ++i) L->c[i] = s.center[i];
+      L->radius = s.size;
+      L->r2 = s.size * s.size;
+      L->r_eps = s.size + EPS;
+      break;
+    }
+    case SHAPE_PLANE: {                                         // math_shapes.rs:154-156
+      L->kind = RT_N_PLANE;
+      plane_into(s.t, s.normal[0], s.normal[1], s.normal[2], s.distance, L->pl[0], L->pn[0]);
+      V pn = normalized({s.normal[0], s.normal[1], s.normal[2]});   // intersects (:169)
+      L->pnorm[0] = pn.x; L->pnorm[1] = pn.y; L->pnorm[2] = pn.z;
+      break;
+    }
+    case SHAPE_CUBE: {                                          // math_shapes.rs:228-244
+      L->kind = RT_N_CUBE;
+      double length = s.size / 2.0;
+      const double* c = s.center;
+      for (int i = 0; i < 3; ++i) {
+        L->c[i] = c[i];
+        L->lo[i] = c[i] - length;
+        L->hi[i] = c[i] + length;
+        L->lo_e[i] = c[i] - length - EPS;
+        L->hi_e[i] = c[i] + length + EPS;
+      }
+      L->radius = length;
+      // stored in get_normal order p1..p6 (:298-305); note the planes sit at +-length/2 (quirk)
+      plane_into(s.t, 0.0, 0.0, 1.0, -(c[2] + length / 2.0), L->pl[0], L->pn[0]);   // p1
+      plane_into(s.t, 0.0, 1.0, 0.0, -(c[1] + length / 2.0), L->pl[1], L->pn[1]);   // p2
+      plane_into(s.t, 1.0, 0.0, 0.0, -(c[0] + length / 2.0), L->pl[2], L->pn[2]);   // p3
+      plane_into(s.t, -1.0, 0.0, 0.0, c[0] + -length / 2.0, L->pl[3], L->pn[3]);    // p4
+      plane_into(s.t, 0.0, -1.0, 0.0, c[1] + -length / 2.0, L->pl[4], L->pn[4]);    // p5
+      plane_into(s.t, 0.0, 0.0, -1.0, c[2] + -length / 2.0, L->pl[5], L->pn[5]);    // p6
+      break;
+    }
+    default:
+      return fail(RT_ERR_INVALID, "internal: make_leaf on CSG");
+  }
+  return RT_OK;
+}
+
+struct Flattener {
+  const rt_scene& s;
+  FlatScene& f;
+  int32_t node_begin = 0;
+  std::vector<int32_t> leaf_node;      // per leaf (object-relative): node index
+  std::vector<int32_t> parent;         // per node (object-relative): parent node or -1
+  int depth_guard = 0;
+
+  // Emit the subtree of shape id `sid`; returns its object-relative node index.
+  int32_t emit(int32_t sid, int* err) {
+    if (sid < 0 || sid >= (int32_t)s.shapes.size()) { *err = fail(RT_ERR_INVALID, "bad shape id %d", sid); return -1; }
+    if (++depth_guard > 64) { *err = fail(RT_ERR_UNSUPPORTED, "CSG nesting deeper than 64"); return -1; }
+    const ShapeRec& r = s.shapes[sid];
+    RtNode n;
+    memset(&n, 0, sizeof n);
+    if (r.kind == SHAPE_CSG) {
+      int32_t a = emit(r.a, err);
+      if (*err) return -1;
+      int32_t b = emit(r.b, err);
+      if (*err) return -1;
+      n.kind = r.op == RT_CSG_UNION ? RT_N_UNION : r.op == RT_CSG_INTERSECTION ? RT_N_INTERSECTION : RT_N_DIFFERENCE;
+      n.a = a; n.b = b; n.leaf = -1;
+    } else {
+      RtLeaf L;
+      int rc = make_leaf(r, &L);
+      if (rc) { *err = rc; return -1; }
+      n.kind = L.kind; n.a = n.b = -1;
+      n.leaf = (int32_t)f.leaves.size();
+      f.leaves.push_back(L);
+    }
+    --depth_guard;
+    int32_t idx = (int32_t)f.nodes.size() - node_begin;
+    f.nodes.push_back(n);
+    parent.push_back(-1);
+    if (n.kind >= RT_N_UNION) { parent[n.a] = idx; parent[n.b] = idx; }
+    return idx;
+  }
+
+  // postfix is_inside of subtree rooted at object-relative node `ni` (csg.rs:126-135)
+  void emit_inside(int32_t ni) {
+    const RtNode& n = f.nodes[node_begin + ni];
+    if (n.kind < RT_N_UNION) { f.prog.push_back({RT_OP_INSIDE, n.leaf}); return; }
+    emit_inside(n.a);
+    emit_inside(n.b);
+    int32_t op = n.kind == RT_N_UNION ? RT_OP_OR : n.kind == RT_N_INTERSECTION ? RT_OP_AND : RT_OP_ANDNOT;
+    f.prog.push_back({op, 0});
+  }
+};
+
+int flatten(const rt_scene& s, FlatScene* out) {
+  FlatScene& f = *out;
+  f = FlatScene();
+  f.width = (int32_t)s.width;
+  f.height = (int32_t)s.height;
+  f.max_depth = s.max_depth;
+  f.any_transparent = 0;
+  f.shadow_early_out = 1;
+  for (const ObjectRec& o : s.objects) {
+    Flattener fl{s, f};
+    fl.node_begin = (int32_t)f.nodes.size();
+    RtObject ob;
+    memset(&ob, 0, sizeof ob);
+    ob.node_begin = fl.node_begin;
+    ob.leaf_begin = (int32_t)f.leaves.size();
+    int err = 0;
+    fl.emit(o.shape, &err);
+    if (err) return err;
+    ob.node_count = (int32_t)f.nodes.size() - ob.node_begin;
+    ob.leaf_count = (int32_t)f.leaves.size() - ob.leaf_begin;
+    if (ob.node_count > 32) return fail(RT_ERR_UNSUPPORTED, "object with %d CSG nodes (max 32)", ob.node_count);
+    // Hit-filter program per leaf: for every CSG ancestor, the sibling's is_inside test with
+    // the polarity of csg.rs:43-95 (Union: !in, !in; Intersection: in, in; Difference: !in, in).
+    for (int32_t ni = 0; ni < ob.node_count; ++ni) {
+      const RtNode& n = f.nodes[ob.node_begin + ni];
+      if (n.kind >= RT_N_UNION) continue;
+      RtLeaf& L = f.leaves[n.leaf];
+      L.prog_begin = (int32_t)f.prog.size();
+      int32_t child = ni, par = fl.parent[ni];
+      while (par >= 0) {
+        const RtNode& P = f.nodes[ob.node_begin + par];
+        bool is_a = P.a == child;
+        int32_t sib = is_a ? P.b : P.a;
+        int want = P.kind == RT_N_INTERSECTION ? 1 : P.kind == RT_N_UNION ? 0 : (is_a ? 0 : 1);
+        fl.emit_inside(sib);
+        f.prog.push_back({RT_OP_REQUIRE, want});
+        child = par;
+        par = fl.parent[par];
+      }
+      f.leaves[n.leaf].prog_end = (int32_t)f.prog.size();
+      (void)L;
+    }
+    const rt_material& m = o.mat;
+    ob.textured = m.texture >= 0;
+    ob.tex = m.texture >= 0 ? m.texture : 0;
+    if (m.texture >= (int32_t)s.textures.size()) return fail(RT_ERR_INVALID, "bad texture id %d", m.texture);
+    ob.color[0] = m.color[0]; ob.color[1] = m.color[1]; ob.color[2] = m.color[2];
+    ob.reflectivity = m.reflectivity;
+    ob.transparency = m.transparency;
+    ob.shadow_skip = m.transparency == 1.0;
+    if (m.transparency != 0.0) f.any_transparent = 1;
+    if (!isfinite(m.transparency)) f.shadow_early_out = 0;
+    f.objects.push_back(ob);
+  }
+  for (const LightRec& l : s.lights) {
+    RtLight L;
+    for (int i = 0; i < 3; ++i) { L.p[i] = l.p[i]; L.col[i] = l.color[i]; }
+    f.lights.push_back(L);
+  }
+  int64_t off = 0;
+  for (const TextureRec& t : s.textures) {
+    RtTexture T;
+    T.offset = off; T.w = (int32_t)t.w; T.h = (int32_t)t.h;
+    f.textures.push_back(T);
+    f.texels.insert(f.texels.end(), t.rgba.begin(), t.rgba.end());
+    off += (int64_t)t.rgba.size();
+    while (off % 16) { f.texels.push_back(0); ++off; }
+  }
+  // PerspectiveCamera::new(width, height, center, None, None, None) (camera.rs:30-54)
+  V center = {s.cam_center[0], s.cam_center[1], s.cam_center[2]};
+  V look_at = {0.0, 0.0, 0.0}, up = {0.0, 1.0, 0.0}, right = {0.0, 0.0, 0.0};
+  V direction = normalized(sub(look_at, center));
+  double aspect = (double)s.width / (double)s.height;
+  if (length(right) == 0.0) { V c = cross(direction, up); right = {-c.x, -c.y, -c.z}; }
+  RtCamera& cam = f.cam;
+  cam.center[0] = center.x; cam.center[1] = center.y; cam.center[2] = center.z;
+  cam.direction[0] = direction.x; cam.direction[1] = direction.y; cam.direction[2] = direction.z;
+  cam.right[0] = right.x; cam.right[1] = right.y; cam.right[2] = right.z;
+  cam.up[0] = up.x; cam.up[1] = up.y; cam.up[2] = up.z;
+  cam.aspect = aspect;
+  cam.width = (double)s.width;
+  cam.height = (double)s.height;
+  return RT_OK;
+}
+
+}  // namespace rt
+
+using namespace rt;
+
+// ==================================================================== C ABI: construction
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_xform_identity(rt_transformation* out) {
+  if (!out) return fail(RT_ERR_INVALID, "null output");
+  xf_identity(out);
+  return RT_OK;
+}
+int rt_xform_translation(double x, double y, double z, rt_transformation* out) {
+  if (!out) return fail(RT_ERR_INVALID, "null output");
+  xf_translation(x, y, z, out);
+  return RT_OK;
+}
+int rt_xform_rotation(double x, double y, double z, rt_transformation* out) {
+  if (!out) return fail(RT_ERR_INVALID, "null output");
+  xf_rotation(x, y, z, out);
+  return RT_OK;
+}
+int rt_xform_scaling(double x, double y, double z, rt_transformation* out) {
+  if (!out) return fail(RT_ERR_INVALID, "null output");
+  xf_scaling(x, y, z, out);
+  return RT_OK;
+}
+int rt_xform_compose(const rt_transformation* self_, const rt_transformation* other, rt_transformation* out) {
+  if (!self_ || !other || !out) return fail(RT_ERR_INVALID, "null argument");
+  xf_compose(*self_, *other, out);
+  return RT_OK;
+}
+
+int rt_scene_new(uint32_t width, uint32_t height, rt_scene** out) {
+  if (!out) return fail(RT_ERR_INVALID, "null output");
+  *out = nullptr;
+  if (width == 0 || height == 0 || width > 65536 || height > 65536)
+    return fail(RT_ERR_INVALID, "bad frame size %ux%u", width, height);
+  rt_scene* s = new (std::nothrow) rt_scene();
+  if (!s) return fail(RT_ERR_NOMEM, "out of memory");
+  s->width = width;
+  s->height = height;
+  *out = s;
+  return RT_OK;
+}
+
+int rt_scene_add_test_objects(rt_scene* s) {                     // raytracer.rs:125-129
+  if (!s) return fail(RT_ERR_INVALID, "null scene");
+  LightRec l;
+  l.p[0] = -10.0; l.p[1] = 30.0; l.p[2] = -50.0;
+  l.color[0] = l.color[1] = l.color[2] = 0.5; l.color[3] = 1.0;   // Color::in_range(0.5, 0.5, 0.5)
+  l.fade = 100.0;
+  s->lights.push_back(l);
+  return RT_OK;
+}
+
+int rt_scene_add_texture(rt_scene* s, uint32_t w, uint32_t h, const uint8_t* rgba8) {
+  if (!s || !rgba8) return fail(RT_ERR_INVALID, "null argument");
+  if (w == 0 || h == 0 || (uint64_t)w * h > (1ull << 28)) return fail(RT_ERR_INVALID, "bad texture size");
+  TextureRec t;
+  t.w = w; t.h = h;
+  t.rgba.assign(rgba8, rgba8 + (size_t)w * h * 4);
+  s->textures.push_back(std::move(t));
+  return (int)s->textures.size() - 1;
+}
+
+static int add_shape(rt_scene* s, const ShapeRec& r) {
+  s->shapes.push_back(r);
+  return (int)s->shapes.size() - 1;
+}
+
+int rt_shape_sphere(rt_scene* s, const rt_transformation* t, const double c[3], double radius) {
+  if (!s || !t || !c) return fail(RT_ERR_INVALID, "null argument");
+  ShapeRec r;
+  memset(&r, 0, sizeof r);
+  r.kind = SHAPE_SPHERE; r.t = *t;
+  memcpy(r.center, c, sizeof r.center);
+  r.size = radius;
+  return add_shape(s, r);
+}
+int rt_shape_cube(rt_scene* s, const rt_transformation* t, const double c[3], double length) {
+  if (!s || !t || !c) return fail(RT_ERR_INVALID, "null argument");
+  ShapeRec r;
+  memset(&r, 0, sizeof r);
+  r.kind = SHAPE_CUBE; r.t = *t;
+  memcpy(r.center, c, sizeof r.center);
+  r.size = length;
+  return add_shape(s, r);
+}
+int rt_shape_plane(rt_scene* s, const rt_transformation* t, const double n[3], double distance) {
+  if (!s || !t || !n) return fail(RT_ERR_INVALID, "null argument");
+  ShapeRec r;
+  memset(&r, 0, sizeof r);
+  r.kind = SHAPE_PLANE; r.t = *t;
+  memcpy(r.normal, n, sizeof r.normal);
+  r.distance = distance;
+  return add_shape(s, r);
+}
+int rt_shape_csg(rt_scene* s, rt_csg_op op, int32_t a, int32_t b) {
+  if (!s) return fail(RT_ERR_INVALID, "null scene");
+  if (a < 0 || b < 0 || a >= (int32_t)s->shapes.size() || b >= (int32_t)s->shapes.size())
+    return fail(RT_ERR_INVALID, "bad CSG child id");
+  if (op != RT_CSG_UNION && op != RT_CSG_INTERSECTION && op != RT_CSG_DIFFERENCE)
+    return fail(RT_ERR_INVALID, "bad CSG operator %d", (int)op);
+  ShapeRec r;
+  memset(&r, 0, sizeof r);
+  r.kind = SHAPE_CSG; r.op = op; r.a = a; r.b = b;
+  xf_identity(&r.t);
+  return add_shape(s, r);
+}
+int rt_scene_add_object(rt_scene* s, int32_t shape, const rt_material* m) {
+  if (!s || !m) return fail(RT_ERR_INVALID, "null argument");
+  if (shape < 0 || shape >= (int32_t)s->shapes.size()) return fail(RT_ERR_INVALID, "bad shape id %d", shape);
+  if (m->texture >= (int32_t)s->textures.size()) return fail(RT_ERR_INVALID, "bad texture id %d", m->texture);
+  s->objects.push_back({shape, *m});
+  return RT_OK;
+}
+int rt_scene_add_light(rt_scene* s, const double p[3], const double col[4], double fade) {
+  if (!s || !p || !col) return fail(RT_ERR_INVALID, "null argument");
+  LightRec l;
+  memcpy(l.p, p, sizeof l.p);
+  memcpy(l.color, col, sizeof l.color);
+  l.fade = fade;
+  s->lights.push_back(l);
+  return RT_OK;
+}
+int rt_scene_set_camera(rt_scene* s, const double c[3]) {
+  if (!s || !c) return fail(RT_ERR_INVALID, "null argument");
+  memcpy(s->cam_center, c, sizeof s->cam_center);
+  return RT_OK;
+}
+int rt_scene_set_max_depth(rt_scene* s, int32_t d) {
+  if (!s) return fail(RT_ERR_INVALID, "null scene");
+  if (d < 0) return fail(RT_ERR_INVALID, "negative max_depth");
+  if (d > RT_MAX_DEPTH_CAP) return fail(RT_ERR_UNSUPPORTED, "max_depth %d > %d", d, RT_MAX_DEPTH_CAP);
+  s->max_depth = d;
+  return RT_OK;
+}
+int rt_scene_info(const rt_scene* s, int32_t* n_objects, int32_t* n_lights, int32_t* n_leaves,
+                  uint32_t* width, uint32_t* height) {
+  if (!s) return fail(RT_ERR_INVALID, "null scene");
+  if (n_objects) *n_objects = (int32_t)s->objects.size();
+  if (n_lights) *n_lights = (int32_t)s->lights.size();
+  if (n_leaves) {
+    FlatScene f;
+    int rc = flatten(*s, &f);
+    if (rc) return rc;
+    *n_leaves = (int32_t)f.leaves.size();
+  }
+  if (width) *width = s->width;
+  if (height) *height = s->height;
+  return RT_OK;
+}
+void rt_scene_free(rt_scene* s) { delete s; }
+
+int rt_scene_compile(const char* text, const char* asset_dir, double time, uint32_t width,
+                     uint32_t height, rt_scene** out) {
+  if (!text || !out) return fail(RT_ERR_INVALID, "null argument");
+  *out = nullptr;
+  rt_scene* s = nullptr;
+  int rc = rt_scene_new(width, height, &s);
+  if (rc) return rc;
+  rt_scene_add_test_objects(s);                                 // debug_window.rs:54-55
+  rc = compile_scene_text(text, asset_dir, time, s);
+  if (rc == RT_OK) { *out = s; return RT_OK; }
+  if (rc == RT_ERR_PARSE) {                                     // default scene, error reported
+    std::string msg = rt_last_error();
+    rt_scene_free(s);
+    rt_scene_new(width, height, &s);
+    rt_scene_add_test_objects(s);
+    *out = s;
+    set_error_message(msg);
+    return RT_ERR_PARSE;
+  }
+  rt_scene_free(s);
+  return rc;
+}
+
+const char* rt_last_error(void) { return g_last_error.c_str(); }
+
+}  // extern "C"

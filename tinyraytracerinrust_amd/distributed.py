@@ -1,0 +1,84 @@
+"""Multi-GPU frame assembly: row tiles rendered per rank, one all-gather (RCCL over xGMI).
+
+The reference renders a frame as one thread-pool job (src/raydebugger/gui.rs:677,
+debug_window.rs:229-273) and has no distributed code.  Pixels are independent, so the frame
+is split into equal row tiles, one per rank (one process per GPU); each rank renders its tile
+with the HIP kernel and a single ``all_gather_into_tensor`` (backend "nccl" = RCCL) assembles
+the RGBA8 frame on every rank.  Two tilings:
+
+* ``contiguous``: rank r owns rows [r*T, (r+1)*T), T = ceil(H/G) (last tile padded);
+* ``cyclic``: bands of ``band`` rows dealt round-robin (band b -> rank b % G), which evens out
+  the sky-vs-floor cost imbalance; the gathered buffer is reordered locally afterwards.
+
+The same functions run on CPU tensors under ``gloo`` (tests/test_distributed_gloo.py), with a
+caller-supplied ``render_rows(y0, y1, out)`` instead of the GPU renderer.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def contiguous_rows(height: int, world: int, rank: int) -> List[Tuple[int, int]]:
+    tile = -(-height // world)
+    y0 = min(height, rank * tile)
+    return [(y0, min(height, y0 + tile))]
+
+
+def cyclic_rows(height: int, world: int, rank: int, band: int) -> List[Tuple[int, int]]:
+    out = []
+    nb = -(-height // band)
+    for b in range(rank, nb, world):
+        out.append((b * band, min(height, (b + 1) * band)))
+    return out
+
+
+def rows_per_rank(height: int, world: int, layout: str, band: int) -> int:
+    """Rows in every rank's (padded) slot of the gather buffer; equal for all ranks."""
+    if layout == "contiguous":
+        return -(-height // world)
+    nb = -(-height // band)
+    return -(-nb // world) * band
+
+
+def owned_rows(height: int, world: int, rank: int, layout: str = "contiguous", band: int = 16):
+    return contiguous_rows(height, world, rank) if layout == "contiguous" else cyclic_rows(height, world, rank, band)
+
+
+def render_local(render_rows: Callable[[int, int, torch.Tensor], None], height: int, width: int, world: int,
+                 rank: int, layout: str, band: int, device, dtype=torch.uint8) -> torch.Tensor:
+    """This rank's slot: its rows packed densely (padding rows left zero)."""
+    slot = torch.zeros((rows_per_rank(height, world, layout, band), width, 4), dtype=dtype, device=device)
+    r = 0
+    for y0, y1 in owned_rows(height, world, rank, layout, band):
+        render_rows(y0, y1, slot[r:r + (y1 - y0)])
+        r += y1 - y0
+    return slot
+
+
+def assemble(gathered: torch.Tensor, height: int, world: int, layout: str, band: int) -> torch.Tensor:
+    """gathered: (world * slot_rows, W, 4) in rank order -> (H, W, 4) frame."""
+    slot_rows = gathered.shape[0] // world
+    if layout == "contiguous":
+        return gathered[:height]
+    frame = torch.empty((height,) + tuple(gathered.shape[1:]), dtype=gathered.dtype, device=gathered.device)
+    for rank in range(world):
+        r = rank * slot_rows
+        for y0, y1 in cyclic_rows(height, world, rank, band):
+            frame[y0:y1] = gathered[r:r + (y1 - y0)]
+            r += y1 - y0
+    return frame
+
+
+def render_frame_distributed(render_rows: Callable[[int, int, torch.Tensor], None], height: int, width: int,
+                             device, layout: str = "contiguous", band: int = 16, group=None,
+                             assemble_frame: bool = True) -> torch.Tensor:
+    """Render this rank's rows, all-gather every slot, return the (H, W, 4) RGBA8 frame."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    slot = render_local(render_rows, height, width, world, rank, layout, band, device)
+    gathered = torch.empty((world * slot.shape[0], width, 4), dtype=slot.dtype, device=slot.device)
+    dist.all_gather_into_tensor(gathered, slot, group=group)
+    return assemble(gathered, height, world, layout, band) if assemble_frame else gathered

@@ -1,0 +1,349 @@
+"""Host-side mirror of the reference's render-path interface, over the C ABI.
+
+Mirrors the names and argument meaning of the reference (andreivasiliu/TinyRaytracerInRust):
+
+* ``MatrixTransformation`` / ``TransformationStack``  -- src/raytracer/transformation.rs:7-205
+* ``RayTracer``  -- src/raytracer/raytracer.rs:21-364 (new_default, add_test_objects, add_object,
+  add_light, set_camera_from_vector, get_pixel, max_depth) plus the DebugWindow row loop
+  ``render_lines`` (src/raydebugger/debug_window.rs:74-87) and ``load_scene``
+  (src/sceneparser/scene_loader.rs:24-47, as reached from debug_window.rs:53-62).
+
+Everything renders on the GPU through librt_mi355x.so; there is no CPU path.  Device buffers are
+torch tensors (``torch`` is plumbing for HBM allocations and streams), host results are numpy.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, Iterator, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, d3, d4, lib
+
+MAX_FRAMES = 300   # src/raydebugger/gui.rs:20 -- the GUI's time = frame / MAX_FRAMES
+
+
+class MatrixTransformation:
+    """transformation.rs:47-205: a 4x4 matrix and its separately built inverse."""
+
+    def __init__(self, xf: Optional[_lib.rt_transformation] = None):
+        self.xf = xf if xf is not None else _lib.rt_transformation()
+        if xf is None:
+            check(lib().rt_xform_identity(ctypes.byref(self.xf)))
+
+    @classmethod
+    def create_identity_matrix(cls) -> "MatrixTransformation":
+        return cls()
+
+    @classmethod
+    def _make(cls, fn, x, y, z) -> "MatrixTransformation":
+        t = _lib.rt_transformation()
+        check(fn(float(x), float(y), float(z), ctypes.byref(t)))
+        return cls(t)
+
+    @classmethod
+    def create_translation_matrix(cls, x, y, z):
+        return cls._make(lib().rt_xform_translation, x, y, z)
+
+    @classmethod
+    def create_rotation_matrix(cls, x, y, z):
+        return cls._make(lib().rt_xform_rotation, x, y, z)
+
+    @classmethod
+    def create_scaling_matrix(cls, x, y, z):
+        return cls._make(lib().rt_xform_scaling, x, y, z)
+
+    def compose_with(self, other: "MatrixTransformation") -> "MatrixTransformation":
+        out = _lib.rt_transformation()
+        check(lib().rt_xform_compose(ctypes.byref(self.xf), ctypes.byref(other.xf), ctypes.byref(out)))
+        return MatrixTransformation(out)
+
+    @property
+    def matrix(self) -> np.ndarray:
+        return np.array(self.xf.matrix[:]).reshape(4, 4)
+
+    @property
+    def inverse_matrix(self) -> np.ndarray:
+        return np.array(self.xf.inverse[:]).reshape(4, 4)
+
+    def transform_vector(self, v: Sequence[float]) -> np.ndarray:
+        """transformation.rs:53-59, left-to-right sums."""
+        m = self.xf.matrix
+        x, y, z = (float(c) for c in v)
+        return np.array([m[4 * r] * x + m[4 * r + 1] * y + m[4 * r + 2] * z + m[4 * r + 3] for r in range(3)])
+
+
+class TransformationStack:
+    """transformation.rs:7-37."""
+
+    def __init__(self):
+        self.stack = [MatrixTransformation.create_identity_matrix()]
+
+    def push_transformation(self, t: MatrixTransformation) -> None:
+        self.stack.append(t.compose_with(self.stack[-1]) if self.stack else t)
+
+    def pop_transformation(self) -> MatrixTransformation:
+        if not self.stack:
+            raise IndexError("Trying to pop from an empty TransformationStack!")
+        return self.stack.pop()
+
+    def get_transformation(self) -> MatrixTransformation:
+        return self.stack[-1]
+
+
+def solid_material(color=(0.0, 0.0, 0.0, 1.0), reflectivity=0.0, transparency=0.0) -> _lib.rt_material:
+    """SolidColorMaterial::new (material.rs:41-49); RTObject::new's default is BLACK (rt_object.rs:13-20)."""
+    c = list(color) + [1.0] * (4 - len(color))
+    return _lib.rt_material(d4(c), -1, float(reflectivity), float(transparency))
+
+
+def textured_material(texture_id: int, reflectivity=0.0, transparency=0.0) -> _lib.rt_material:
+    """TexturedMaterial::new (material.rs:76-84)."""
+    return _lib.rt_material(d4((0, 0, 0, 1)), int(texture_id), float(reflectivity), float(transparency))
+
+
+class Scene:
+    """Owner of an ``rt_scene*`` (the RayTracer's scene content)."""
+
+    def __init__(self, handle: int, width: int, height: int, status: int = 0, error: str = ""):
+        self.h = ctypes.c_void_p(handle)
+        self.width, self.height = width, height
+        self.status, self.error = status, error
+
+    @classmethod
+    def new_default(cls, width: int, height: int) -> "Scene":
+        h = ctypes.c_void_p()
+        check(lib().rt_scene_new(width, height, ctypes.byref(h)))
+        return cls(h.value, width, height)
+
+    @classmethod
+    def compile(cls, text: str, time: float, width: int, height: int,
+                asset_dir: Optional[str] = None, strict: bool = True) -> "Scene":
+        """load_scene on a fresh new_default()+add_test_objects() RayTracer.
+
+        A parse error raises when ``strict``; otherwise the default scene is returned with
+        ``status``/``error`` set, as the reference prints the error and renders on
+        (debug_window.rs:58-60)."""
+        h = ctypes.c_void_p()
+        rc = lib().rt_scene_compile(text.encode(), asset_dir.encode() if asset_dir else None,
+                                    float(time), width, height, ctypes.byref(h))
+        if rc == -2 and not strict and h.value:
+            return cls(h.value, width, height, rc, lib().rt_last_error().decode())
+        check(rc)
+        return cls(h.value, width, height)
+
+    def info(self) -> dict:
+        no, nl, nlf = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        w, h = ctypes.c_uint32(), ctypes.c_uint32()
+        check(lib().rt_scene_info(self.h, ctypes.byref(no), ctypes.byref(nl), ctypes.byref(nlf),
+                                  ctypes.byref(w), ctypes.byref(h)))
+        return {"objects": no.value, "lights": nl.value, "leaves": nlf.value,
+                "width": w.value, "height": h.value}
+
+    def free(self) -> None:
+        if self.h and self.h.value:
+            lib().rt_scene_free(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Renderer:
+    """Owner of an ``rt_ctx*``: one device, its stream, the uploaded scene."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        check(lib().rt_ctx_create(int(device), ctypes.byref(h)))
+        self.h = h
+        self.device = device
+        self.width = self.height = 0
+
+    def upload(self, scene: Scene) -> None:
+        check(lib().rt_ctx_upload(self.h, scene.h))
+        self.width, self.height = scene.width, scene.height
+
+    def render_rows_into(self, y0: int, y1: int, out_ptr: int, row_stride: int, max_depth: int = -1,
+                         stream: Optional[int] = None, f64: bool = False) -> None:
+        fn = lib().rt_render_rows_f64 if f64 else lib().rt_render_rows
+        check(fn(self.h, y0, y1, max_depth, ctypes.c_void_p(out_ptr), row_stride,
+                 ctypes.c_void_p(stream) if stream else None))
+
+    def render_rows(self, y0: int, y1: int, max_depth: int = -1, f64: bool = False, out=None,
+                    stream=None):
+        """Render rows [y0, y1) into a device tensor (torch, on this device) and return it.
+
+        uint8 RGBA (rows, W, 4) by default, float64 RGBA with ``f64``.  Runs on ``stream``
+        (a torch.cuda.Stream) or torch's current stream, asynchronously."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        if out is None:
+            out = torch.empty((y1 - y0, self.width, 4), dtype=torch.float64 if f64 else torch.uint8, device=dev)
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        self.render_rows_into(y0, y1, out.data_ptr(), out.stride(0) * out.element_size(), max_depth,
+                              st.cuda_stream, f64)
+        return out
+
+    def render_rows_host(self, y0: int, y1: int, max_depth: int = -1, f64: bool = False) -> np.ndarray:
+        """Synchronous render into a host numpy array (the library stages through HBM)."""
+        out = np.empty((y1 - y0, self.width, 4), np.float64 if f64 else np.uint8)
+        self.render_rows_into(y0, y1, out.ctypes.data, out.strides[0], max_depth, None, f64)
+        return out
+
+    def render_points(self, xy: np.ndarray, max_depth: int = -1) -> np.ndarray:
+        xy = np.ascontiguousarray(xy, dtype=np.float64).reshape(-1, 2)
+        out = np.empty((xy.shape[0], 4), np.float64)
+        check(lib().rt_render_points_f64(self.h, ctypes.c_void_p(xy.ctypes.data), xy.shape[0], max_depth,
+                                         ctypes.c_void_p(out.ctypes.data), None))
+        return out
+
+    def last_kernel_ms(self) -> float:
+        ms = ctypes.c_float()
+        check(lib().rt_ctx_last_kernel_ms(self.h, ctypes.byref(ms)))
+        return ms.value
+
+    def synchronize(self) -> None:
+        check(lib().rt_ctx_synchronize(self.h))
+
+    def free(self) -> None:
+        if self.h and self.h.value:
+            lib().rt_ctx_free(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class RayTracer:
+    """raytracer.rs:21-364 over the GPU path.
+
+    Build the scene with the same calls the reference's scene parser makes, or ``load_scene``
+    a DSL text; then ``get_pixel`` / ``render_lines`` as the GUI worker does."""
+
+    def __init__(self, width: int, height: int, device: int = 0):
+        self.width, self.height = width, height
+        self.scene = Scene.new_default(width, height)       # RayTracer::new_default (:38-44)
+        self.transformation_stack = TransformationStack()
+        self.device = device
+        self._renderer: Optional[Renderer] = None
+        self._dirty = True
+        self._max_depth = 10
+
+    new_default = classmethod(lambda cls, width, height, device=0: cls(width, height, device))
+
+    # -- scene construction (raytracer.rs:72-130, 289-330) --------------------------------
+    def add_test_objects(self) -> None:
+        check(lib().rt_scene_add_test_objects(self.scene.h))
+        self._dirty = True
+
+    def add_texture(self, rgba8: np.ndarray) -> int:
+        rgba8 = np.ascontiguousarray(rgba8, dtype=np.uint8)
+        h, w = rgba8.shape[:2]
+        self._dirty = True
+        return check(lib().rt_scene_add_texture(self.scene.h, w, h, ctypes.c_void_p(rgba8.ctypes.data)))
+
+    def _xf(self, t: Optional[MatrixTransformation]) -> _lib.rt_transformation:
+        return (t or self.transformation_stack.get_transformation()).xf
+
+    def sphere(self, center=(0, 0, 0), radius=1.0, t: Optional[MatrixTransformation] = None) -> int:
+        return check(lib().rt_shape_sphere(self.scene.h, ctypes.byref(self._xf(t)), d3(center), float(radius)))
+
+    def cube(self, center=(0, 0, 0), length=1.0, t: Optional[MatrixTransformation] = None) -> int:
+        return check(lib().rt_shape_cube(self.scene.h, ctypes.byref(self._xf(t)), d3(center), float(length)))
+
+    def plane(self, normal=(0, 1, 0), distance=1.0, t: Optional[MatrixTransformation] = None) -> int:
+        return check(lib().rt_shape_plane(self.scene.h, ctypes.byref(self._xf(t)), d3(normal), float(distance)))
+
+    def csg(self, a: int, b: int, operator: str = "union") -> int:
+        op = {"union": 0, "intersection": 1, "difference": 2}[operator]
+        return check(lib().rt_shape_csg(self.scene.h, op, a, b))
+
+    def add_object(self, shape: int, material: Optional[_lib.rt_material] = None) -> None:
+        check(lib().rt_scene_add_object(self.scene.h, shape, ctypes.byref(material or solid_material())))
+        self._dirty = True
+
+    def add_light(self, point, color=(0.5, 0.5, 0.5, 1.0), fade_distance=100.0) -> None:
+        check(lib().rt_scene_add_light(self.scene.h, d3(point), d4(list(color) + [1.0] * (4 - len(color))),
+                                       float(fade_distance)))
+        self._dirty = True
+
+    def set_camera_from_vector(self, center) -> None:
+        """raytracer.rs:289-299: the centre is transformed by the stack top first."""
+        c = self.transformation_stack.get_transformation().transform_vector(center)
+        check(lib().rt_scene_set_camera(self.scene.h, d3(c)))
+        self._dirty = True
+
+    @property
+    def max_depth(self) -> int:
+        return self._max_depth
+
+    @max_depth.setter
+    def max_depth(self, d: int) -> None:
+        check(lib().rt_scene_set_max_depth(self.scene.h, int(d)))
+        self._max_depth = int(d)
+        self._dirty = True
+
+    def load_scene(self, text: str, time: float = 0.0, asset_dir: Optional[str] = None,
+                   strict: bool = True) -> None:
+        """DebugWindow::load_ray_tracer (debug_window.rs:53-62): a fresh new_default RayTracer
+        with the test light, then load_scene(text, time).  Replaces this tracer's scene."""
+        self.scene = Scene.compile(text, time, self.width, self.height, asset_dir, strict)
+        self.transformation_stack = TransformationStack()
+        if self._max_depth != 10:
+            check(lib().rt_scene_set_max_depth(self.scene.h, self._max_depth))
+        self._dirty = True
+
+    # -- rendering ------------------------------------------------------------------------
+    @property
+    def renderer(self) -> Renderer:
+        if self._renderer is None:
+            self._renderer = Renderer(self.device)
+        if self._dirty:
+            self._renderer.upload(self.scene)
+            self._dirty = False
+        return self._renderer
+
+    def get_pixel(self, x: float, y: float) -> np.ndarray:
+        """raytracer.rs:359-363: colour (r, g, b, a) of the camera ray through (x, y)."""
+        return self.renderer.render_points(np.array([[x, y]], np.float64))[0]
+
+    def render_lines(self, line_range: Iterable[int]) -> Iterator[Tuple[int, np.ndarray]]:
+        """debug_window.rs:74-87: yields (y, row of W colours as (W, 4) f64)."""
+        r = self.renderer
+        for y in line_range:
+            yield y, r.render_rows_host(y, y + 1, f64=True)[0]
+
+    def render_frame(self) -> np.ndarray:
+        """The whole frame as RGBA8 (H, W, 4), quantised as easy_pixbuf.rs:46-53."""
+        return self.renderer.render_rows_host(0, self.height)
+
+
+def write_png(path: str, rgba8: np.ndarray, channels: int = 3) -> None:
+    rgba8 = np.ascontiguousarray(rgba8, dtype=np.uint8)
+    h, w = rgba8.shape[:2]
+    check(lib().rt_write_png(path.encode(), ctypes.c_void_p(rgba8.ctypes.data), w, h, rgba8.strides[0], channels))
+
+
+def read_png_rgba8(path: str) -> np.ndarray:
+    p = ctypes.c_void_p()
+    w, h = ctypes.c_uint32(), ctypes.c_uint32()
+    check(lib().rt_read_png_rgba8(path.encode(), ctypes.byref(p), ctypes.byref(w), ctypes.byref(h)))
+    try:
+        buf = (ctypes.c_uint8 * (w.value * h.value * 4)).from_address(p.value)
+        return np.frombuffer(buf, np.uint8).reshape(h.value, w.value, 4).copy()
+    finally:
+        lib().rt_free_buffer(p)
+
+
+def device_count() -> int:
+    n = ctypes.c_int()
+    check(lib().rt_device_count(ctypes.byref(n)))
+    return n.value
