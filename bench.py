@@ -1,0 +1,256 @@
+#!/usr/bin/env python
+"""bench.py -- Mrays/s of the MI355X render path on the BASELINE workload.
+
+Workload (BASELINE.json metric "Mrays/sec at 3840x2160 globes.scene"; configs[3]):
+globes.scene at t=0, 3840x2160, max_depth 10 (the reference's hard-coded depth,
+raytracer.rs:65), default test light, RGBA8 output.  One step = one frame:
+
+* N = 1: one kernel launch renders all 2160 rows into an HBM framebuffer;
+* N > 1: one process per GPU (torchrun); rank r renders its row tile (contiguous by default,
+  ``--layout cyclic`` deals 16-row bands round-robin) and one RCCL all_gather_into_tensor over
+  xGMI assembles the frame on every rank (cyclic adds a local reorder).  Total work is fixed as
+  N grows: scaling "strong".
+
+value = W*H primary rays per frame * K frames / (max over ranks of the timed wall time), in
+millions.  The scene blob and texture are uploaded before the timed region (inputs resident in
+HBM).  rank 0 prints ONE JSON line with two extra objects:
+
+* roofline -- the render kernel against the FP64 vector roofline (this path has no dense
+  contraction and ~0.1 B/flop, see DESIGN.md "Roofline"): algorithmic flops per launch (the
+  reference algorithm's f64 ops for the rows the launch renders, counted by the oracle's counting
+  build: tests/golden/flops_*.json) / the kernel's mean duration measured here with HIP events on
+  the launch stream; traffic = HBM bytes per launch from the committed rocprofv3 PMC summary
+  (profiles/) when it exists for this workload, else null.  ``roofline_hbm`` restates the same
+  launch against HBM bandwidth, as the north star asks.
+* cpu_baseline -- the CPU oracle (a faithful C restatement of the reference loop; the Rust
+  reference cannot be built here) timed on this host on rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+SCENES = os.path.join(ROOT, "tests", "golden", "scenes")
+
+FP64_VECTOR_PEAK_TFLOPS = 78.6     # MI355X spec, FMA counted as 2 flops
+FP64_NO_FMA_TFLOPS = 39.3          # one add or mul per lane per cycle: the parity-bound ceiling
+HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md chip table (spec)
+
+CONFIGS = {
+    # name: (scene, width, height, time, max_depth)
+    "globes4k": ("globes", 3840, 2160, 0.0, 10),
+    "globes1080d5": ("globes", 1920, 1080, 0.0, 5),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="globes4k", choices=sorted(CONFIGS))
+    ap.add_argument("--layout", default="contiguous", choices=["contiguous", "cyclic"])
+    ap.add_argument("--band", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--png", default="", help="write the rendered frame (rank 0) to this PNG")
+    return ap.parse_args()
+
+
+def owned_rows(H, world, rank, layout, band):
+    from tinyraytracerinrust_amd import distributed as D
+    return D.owned_rows(H, world, rank, layout, band)
+
+
+def load_flops(scene, W, H, t, depth):
+    path = os.path.join(ROOT, "tests", "golden", f"flops_{scene}_{W}x{H}_t{t:g}_d{depth}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def load_traffic(config, world, layout):
+    """HBM bytes per launch of the render kernel from the committed PMC summary (or None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    key = f"{config}/n{world}/{layout}"
+    e = d.get(key) or (d.get(f"{config}/n1/contiguous") if world == 1 else None)
+    return None if e is None else e.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(text, W, H, t, depth, threads):
+    """Time the CPU oracle: all `threads` on the whole frame, and 1 thread on a row sample."""
+    from oracle import oracle as O
+    O.register_texture_file("worldmap.png", os.path.join(SCENES, "worldmap.png"))
+    sc = O.OracleScene(text, t, W, H, max_depth=depth)
+    t0 = time.perf_counter()
+    sc.render(0, H, threads=threads, u8=True)
+    dt_all = time.perf_counter() - t0
+    step = 27
+    rows = len(range(0, H, step))
+    t0 = time.perf_counter()
+    sc.render(0, H, row_step=step, threads=1, u8=True)
+    dt_one = time.perf_counter() - t0
+    return {
+        "value": round(W * H / dt_all / 1e6, 3),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"whole {W}x{H} frame, rows interleaved over {threads} threads "
+                  f"({dt_all * threads:.1f} thread-s of CPU work); oracle/rt_oracle.c -O2 -ffp-contract=off",
+        "single_thread_value": round(rows * W / dt_one / 1e6, 3),
+        "single_thread_sample": f"every {step}th row ({rows} rows x {W} px) on 1 thread",
+    }
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    import tinyraytracerinrust_amd as T
+    from tinyraytracerinrust_amd import distributed as D
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    scene, W, H, t, depth = CONFIGS[a.config]
+    text = open(os.path.join(SCENES, scene + ".scene")).read()
+    rt = T.RayTracer(W, H, device=local)
+    rt.load_scene(text, t, asset_dir=SCENES)
+    rend = rt.renderer                                    # uploads the scene blob + texture
+
+    layout = a.layout if world > 1 else "contiguous"
+    band = a.band if layout == "cyclic" else -(-H // world)
+    slot_rows = D.rows_per_rank(H, world, layout, band)
+    mine = owned_rows(H, world, rank, layout, band)
+    n_bands = len(mine)
+    if layout == "contiguous":
+        y_first, band_rows, pitch = mine[0][0], mine[0][1] - mine[0][0], H
+    else:
+        y_first, band_rows, pitch = mine[0][0], band, world * band
+    frame = torch.zeros((max(H, world * slot_rows), W, 4), dtype=torch.uint8, device=dev)
+    slot = frame if world == 1 else torch.zeros((slot_rows, W, 4), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev0=None, ev1=None):
+        if ev0 is not None:
+            ev0.record(stream)
+        if world == 1:
+            rend.render_rows(0, H, max_depth=depth, out=frame, stream=stream)
+        else:
+            rend.render_row_bands(y_first, band_rows, pitch, n_bands, slot, max_depth=depth, stream=stream)
+        if ev1 is not None:
+            ev1.record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(frame, slot)
+            if layout == "cyclic":
+                D.assemble(frame, H, world, layout, band)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(*evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    kernel_ms = [s.elapsed_time(e) for s, e in evs]
+    mean_kernel_ms = sum(kernel_ms) / len(kernel_ms)
+
+    if rank == 0 and a.png:
+        T.write_png(a.png, frame[:H].cpu().numpy())
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    rows_rendered = [y for (y0, y1) in mine for y in range(y0, y1)]
+    fl = load_flops(scene, W, H, t, depth)
+    flops_launch = sum(fl["row_flops"][y] for y in rows_rendered) if fl else None
+    achieved = flops_launch / (mean_kernel_ms * 1e-3) / 1e12 if flops_launch else None
+    traffic = load_traffic(a.config, world, layout)
+    # algorithmic bytes of one launch: its RGBA8 rows written + scene blob + the texture once
+    alg_bytes = len(rows_rendered) * W * 4 + 1024 * 568 * 4 + 16 * 1024
+    line = {
+        "metric": "Mrays/sec at 3840x2160 globes.scene" if a.config == "globes4k" else f"Mrays/sec {a.config}",
+        "value": round(W * H * a.steps / elapsed / 1e6, 2),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: the reference's own globes.scene + worldmap.png, deterministic (no RNG)",
+        "config": {
+            "workload": f"{scene}.scene {W}x{H} t={t:g} max_depth {depth}, one frame per step",
+            "scene": f"{scene}.scene", "width": W, "height": H, "time": t, "max_depth": depth,
+            "parallelism": f"rowtile{world}" + ("" if world == 1 else f"-{layout}"),
+            "frame_bytes": W * H * 4,
+        },
+        "roofline": {
+            "bound": "fp64-valu",
+            "achieved": round(achieved, 3) if achieved else None,
+            "peak": FP64_VECTOR_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4) if achieved else None,
+            "traffic": traffic,
+            "kernel": "render_rows_kernel",
+            "kernel_ms_mean": round(mean_kernel_ms, 4),
+            "kernel_ms_min": round(min(kernel_ms), 4),
+            "algorithmic_flops_per_launch": flops_launch,
+            "frac_of_no_fma_ceiling": round(achieved / FP64_NO_FMA_TFLOPS, 4) if achieved else None,
+            "no_fma_ceiling": FP64_NO_FMA_TFLOPS,
+        },
+        "roofline_hbm": {
+            "bound": "hbm",
+            "achieved": round(alg_bytes / (mean_kernel_ms * 1e-3) / 1e9, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(alg_bytes / (mean_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "traffic": traffic,
+        },
+        "cpu_baseline": None,
+    }
+    if world == 1 and not a.no_cpu_baseline:
+        cb = cpu_baseline(text, W, H, t, depth, a.cpu_threads)
+        cb["gpu_over_cpu"] = round(line["value"] / cb["value"], 1)
+        line["cpu_baseline"] = cb
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -127,7 +127,15 @@ int rt_ctx_upload(rt_ctx* ctx, const rt_scene* scene);
  * context's scratch and copied back; synchronous).  max_depth < 0 uses the scene's. */
 int rt_render_rows(rt_ctx* ctx, uint32_t y0, uint32_t y1, int32_t max_depth,
                    uint8_t* rgba8, size_t row_stride_bytes, void* stream);
-/* Same, pre-quantisation colours: 4 doubles per pixel (r,g,b,a) -- the `Vec<Color>` rows. */
+/* Band layout for multi-GPU row tiling: n_bands bands of band_rows rows, band b covering
+ * full-frame rows [y_first + b*band_pitch, ... + band_rows) (rows >= H skipped), written
+ * packed: band b row j at output row b*band_rows + j.  A contiguous tile is n_bands = 1; the
+ * cyclic layout of rank r of G uses y_first = r*band_rows, band_pitch = G*band_rows. */
+int rt_render_row_bands(rt_ctx* ctx, uint32_t y_first, uint32_t band_rows, uint32_t band_pitch,
+                        uint32_t n_bands, int32_t max_depth, uint8_t* rgba8, size_t row_stride_bytes,
+                        void* stream);
+/* Same as rt_render_rows, pre-quantisation colours: 4 doubles per pixel (r,g,b,a) -- the
+ * `Vec<Color>` rows. */
 int rt_render_rows_f64(rt_ctx* ctx, uint32_t y0, uint32_t y1, int32_t max_depth,
                        double* rgba_f64, size_t row_stride_bytes, void* stream);
 /* Arbitrary sample positions (the anti-aliaser's fractional get_pixel calls,

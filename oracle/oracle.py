@@ -29,6 +29,7 @@ COUNTER_NAMES = [
     "uv_sphere", "texture_fetch",
     "shade", "light", "light_lit", "shadow_hit", "inside_test",
     "refract_dir", "reflect_dir", "combine",
+    "flop", "transcendental",
 ]
 
 _libs: dict = {}

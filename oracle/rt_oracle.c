@@ -54,16 +54,23 @@ enum {
   C_SHADOW_HIT,         /* transparency multiplications                       */
   C_INSIDE_TEST,        /* angle(-dir, n) per shaded hit                      */
   C_REFRACT_DIR, C_REFLECT_DIR, C_COMBINE,
+  C_FLOP,               /* f64 add/sub/mul/div/sqrt + libm calls, as evaluated by the reference */
+  C_TRANSC,             /* acos / sin calls (also inside C_FLOP)                               */
   C_NUM
 };
 #if ORC_COUNTERS
-static __thread uint64_t *g_cnt;
-#define CNT(e) (g_cnt[(e)]++)
-#define CNTN(e, n) (g_cnt[(e)] += (uint64_t)(n))
+static __thread uint64_t *g_cnt;   /* NULL outside render jobs: scene setup is not counted */
+#define CNT(e) (g_cnt ? (void)(g_cnt[(e)]++) : (void)0)
+#define CNTN(e, n) (g_cnt ? (void)(g_cnt[(e)] += (uint64_t)(n)) : (void)0)
 #else
 #define CNT(e) ((void)0)
 #define CNTN(e, n) ((void)0)
 #endif
+/* FL(n): n floating-point operations evaluated at this point of the reference code.  Negation,
+ * comparisons, clamps and compile-time constants are not counted; sqrt, division and each libm
+ * call count 1 (transcendentals are also tallied in C_TRANSC). */
+#define FL(n) CNTN(C_FLOP, (n))
+#define TR(n) (CNTN(C_FLOP, (n)), CNTN(C_TRANSC, (n)))
 
 /* ------------------------------------------------------------------------- */
 /* math.rs:1-24, vector.rs:3-120                                              */
@@ -76,17 +83,19 @@ typedef struct { Vec point, direction; } Ray;
 typedef struct { double u, v; } UV;
 
 static Vec v_new(double x, double y, double z) { Vec r = {x, y, z}; return r; }
-static Vec v_add(Vec a, Vec b) { return v_new(a.x + b.x, a.y + b.y, a.z + b.z); }   /* vector.rs:70-80 */
-static Vec v_sub(Vec a, Vec b) { return v_new(a.x - b.x, a.y - b.y, a.z - b.z); }   /* vector.rs:82-92 */
-static double v_dot(Vec a, Vec b) { return a.x * b.x + a.y * b.y + a.z * b.z; }     /* vector.rs:94-100 */
-static Vec v_scale(Vec a, double s) { return v_new(a.x * s, a.y * s, a.z * s); }    /* vector.rs:102-112 */
+static Vec v_add(Vec a, Vec b) { FL(3); return v_new(a.x + b.x, a.y + b.y, a.z + b.z); }   /* vector.rs:70-80 */
+static Vec v_sub(Vec a, Vec b) { FL(3); return v_new(a.x - b.x, a.y - b.y, a.z - b.z); }   /* vector.rs:82-92 */
+static double v_dot(Vec a, Vec b) { FL(5); return a.x * b.x + a.y * b.y + a.z * b.z; }     /* vector.rs:94-100 */
+static Vec v_scale(Vec a, double s) { FL(3); return v_new(a.x * s, a.y * s, a.z * s); }    /* vector.rs:102-112 */
 static Vec v_neg(Vec a) { return v_new(-a.x, -a.y, -a.z); }                         /* vector.rs:114-120 */
-static double v_length(Vec a) { return sqrt(v_dot(a, a)); }                         /* vector.rs:49-51 */
-static Vec v_normalized(Vec a) { return v_scale(a, 1.0 / v_length(a)); }            /* vector.rs:45-47 */
+static double v_length(Vec a) { FL(1); return sqrt(v_dot(a, a)); }                         /* vector.rs:49-51 */
+static Vec v_normalized(Vec a) { FL(1); return v_scale(a, 1.0 / v_length(a)); }            /* vector.rs:45-47 */
 static double v_angle(Vec a, Vec b) {                                               /* vector.rs:57-59 */
+  FL(2); TR(1);
   return acos(v_dot(a, b) / (v_length(a) * v_length(b)));
 }
 static Vec v_cross(Vec a, Vec b) {                                                  /* vector.rs:61-67 */
+  FL(9);
   return v_new(a.y * b.z - a.z * b.y, a.x * b.z - a.z * b.x, a.x * b.y - a.y * b.x);
 }
 
@@ -105,9 +114,9 @@ static Color in_range(double r, double g, double b) {                           
   Color c = {in_limit(r, 0.0, 1.0), in_limit(g, 0.0, 1.0), in_limit(b, 0.0, 1.0), 1.0};
   return c;
 }
-static Color c_intensify(Color c, double k) { return in_range(c.r * k, c.g * k, c.b * k); } /* color.rs:71-73 */
-static Color c_mul(Color a, Color b) { return in_range(a.r * b.r, a.g * b.g, a.b * b.b); }  /* color.rs:76-82 */
-static Color c_add(Color a, Color b) { return in_range(a.r + b.r, a.g + b.g, a.b + b.b); }  /* color.rs:84-90 */
+static Color c_intensify(Color c, double k) { FL(3); return in_range(c.r * k, c.g * k, c.b * k); } /* color.rs:71-73 */
+static Color c_mul(Color a, Color b) { FL(3); return in_range(a.r * b.r, a.g * b.g, a.b * b.b); }  /* color.rs:76-82 */
+static Color c_add(Color a, Color b) { FL(3); return in_range(a.r + b.r, a.g + b.g, a.b + b.b); }  /* color.rs:84-90 */
 
 /* Rust `(x * 255.0) as u8`: saturating, truncating, NaN -> 0 (easy_pixbuf.rs:49-52). */
 static uint8_t to_u8(double c) {
@@ -123,6 +132,7 @@ static uint8_t to_u8(double c) {
 typedef struct { double m[4][4]; double inv[4][4]; } Xform;
 
 static Vec transform_vector(Vec v, const double m[4][4]) {                          /* transformation.rs:53-59 */
+  FL(18);
   double a = m[0][0] * v.x + m[0][1] * v.y + m[0][2] * v.z + m[0][3];
   double b = m[1][0] * v.x + m[1][1] * v.y + m[1][2] * v.z + m[1][3];
   double c = m[2][0] * v.x + m[2][1] * v.y + m[2][2] * v.z + m[2][3];
@@ -249,6 +259,7 @@ static size_t f2usize(double v) {
 static Color texture_color_at(const Texture *t, UV uv) {                           /* texture.rs:27-34 */
   double x = uv.u * (double)(t->w - 1);
   double y = (double)t->h - (uv.v * (double)(t->h - 1)) - 1.0;
+  FL(4);
   size_t xi = f2usize(x), yi = f2usize(y);
   CNT(C_TEXTURE_FETCH);
   /* The reference would panic on an out-of-bounds index; clamp instead. */
@@ -299,6 +310,7 @@ static Plane plane_new(Xform t, double a, double b, double c, double d) {       
   return p;
 }
 static int plane_is_transformed_point_on_surface(const Plane *p, Vec q) {           /* :162-164 */
+  FL(6);
   return fabs(p->a * q.x + p->b * q.y + p->c * q.z + p->d) < EPSILON;
 }
 
@@ -323,10 +335,12 @@ static void sphere_intersects(const Shape *s, Ray ray, AddIntersection add, void
   Vec d = v_normalized(ray.direction);
   double scale = 1.0 / v_length(ray.direction);
   double r = s->radius;
+  FL(5);
   double vd = v_dot(v, d);
   double sum = vd * vd - (v_dot(v, v) - r * r);
   if (sum < 0.0) { CNT(C_SPHERE_ISECT_MISS); return; }
   CNT(C_SPHERE_ISECT_HIT);
+  FL(6);
   double first = (-vd + sqrt(sum)) * scale;
   double second = (-vd - sqrt(sum)) * scale;
   add(ctx, first);
@@ -341,11 +355,13 @@ static Vec sphere_get_normal(const Shape *s, Vec p) {                           
 static int sphere_is_inside(const Shape *s, Vec p) {                                /* :70-74 */
   CNT(C_INSIDE_SPHERE);
   Vec q = xf_reverse_transform_vector(&s->t, p);
+  FL(1);
   return v_length(v_sub(q, s->center)) <= s->radius + EPSILON;
 }
 static int sphere_is_on_surface(const Shape *s, Vec p) {                            /* :76-80 */
   CNT(C_ONSURF_SPHERE);
   Vec q = xf_reverse_transform_vector(&s->t, p);
+  FL(1);
   return fabs(v_length(v_sub(q, s->center)) - s->radius) < EPSILON;
 }
 static UV sphere_get_uv(const Shape *s, Vec p) {                                    /* :82-114 */
@@ -355,12 +371,14 @@ static UV sphere_get_uv(const Shape *s, Vec p) {                                
   Vec up = v_new(0.0, 1.0, 0.0);
   Vec u_zero = v_new(0.0, 0.0, -1.0);
   Vec u_qrtr = v_new(-1.0, 0.0, 0.0);
+  TR(1);
   double phi = acos(-(v_dot(up, q)));
   if (isnan(phi)) phi = 0.0;   /* eprintln! + 0.0 (:91-96) */
+  TR(2); FL(3);
   double theta = (acos(v_dot(q, u_zero) / sin(phi))) / (2.0 * PI);
   if (isnan(theta)) theta = 0.0;
   double v = phi / PI;
-  double u = (v_dot(u_qrtr, q) > 0.0) ? 1.0 - theta : theta;
+  double u = (v_dot(u_qrtr, q) > 0.0) ? (FL(1), 1.0 - theta) : theta;
   UV uv = {u, v};
   return uv;
 }
@@ -372,6 +390,7 @@ static void plane_intersects(const Plane *p, Ray ray, AddIntersection add, void 
   Vec r_0 = ray.point, r_d = ray.direction;
   double v_d = v_dot(p_n, r_d);
   if (v_d != 0.0) {
+    FL(3);
     double t = -(v_dot(p_n, r_0) + p->d) * (1.0 / v_d);
     if (t >= 0.0) add(ctx, t);
   }
@@ -400,10 +419,13 @@ static void cube_intersects(const Shape *s, Ray ray, AddIntersection add, void *
   for (int i = 0; i < 3; ++i) {
     if (dv[i] == 0.0) {
       CNT(C_CUBE_ISECT_ZERO_AXIS);
+      FL(1);
+      if (!(pv[i] < cv[i] - s->length)) FL(1);
       if (pv[i] < cv[i] - s->length || pv[i] > cv[i] + s->length) return;
       continue;
     }
     CNT(C_CUBE_ISECT_AXIS);
+    FL(6);
     double t1 = (cv[i] - s->length - pv[i]) / dv[i];
     double t2 = (cv[i] + s->length - pv[i]) / dv[i];
     if (t1 > t2) { double tmp = t1; t1 = t2; t2 = tmp; }
@@ -426,26 +448,29 @@ static Vec cube_get_normal(const Shape *s, Vec p) {                             
 static int cube_is_inside(const Shape *s, Vec p) {                                  /* :319-328 */
   CNT(C_INSIDE_CUBE);
   Vec q = xf_reverse_transform_vector(&s->t, p);
+  FL(6);
   return q.x <= (s->center.x + s->length) && q.x >= (s->center.x - s->length) &&
          q.y <= (s->center.y + s->length) && q.y >= (s->center.y - s->length) &&
          q.z <= (s->center.z + s->length) && q.z >= (s->center.z - s->length);
 }
-static int is_between(double x, double start, double end) { return start <= x && x <= end; } /* :333-335 */
+static int is_between(double x, double start, double end) { return start <= x && x <= end; }
+/* the bound expressions `c - l - EPSILON` / `c + l + EPSILON` are 4 flops per is_between */
+#define BETWEEN(x, lo, hi) (FL(4), is_between((x), (lo), (hi))) /* :333-335 */
 static int cube_is_on_surface(const Shape *s, Vec p) {                              /* :330-355 */
   CNT(C_ONSURF_CUBE);
   Vec q = xf_reverse_transform_vector(&s->t, p);
   Vec c = s->center;
   double l = s->length;
-  if (is_between(q.y, c.y - l - EPSILON, c.y + l + EPSILON) &&
-      is_between(q.x, c.x - l - EPSILON, c.x + l + EPSILON) &&
+  if (BETWEEN(q.y, c.y - l - EPSILON, c.y + l + EPSILON) &&
+      BETWEEN(q.x, c.x - l - EPSILON, c.x + l + EPSILON) &&
       (plane_is_transformed_point_on_surface(&s->p1, q) || plane_is_transformed_point_on_surface(&s->p6, q)))
     return 1;
-  else if (is_between(q.z, c.z - l - EPSILON, c.z + l + EPSILON) &&
-           is_between(q.x, c.x - l - EPSILON, c.x + l + EPSILON) &&
+  else if (BETWEEN(q.z, c.z - l - EPSILON, c.z + l + EPSILON) &&
+           BETWEEN(q.x, c.x - l - EPSILON, c.x + l + EPSILON) &&
            (plane_is_transformed_point_on_surface(&s->p2, q) || plane_is_transformed_point_on_surface(&s->p5, q)))
     return 1;
-  else if (is_between(q.y, c.y - l - EPSILON, c.y + l + EPSILON) &&
-           is_between(q.z, c.z - l - EPSILON, c.z + l + EPSILON) &&
+  else if (BETWEEN(q.y, c.y - l - EPSILON, c.y + l + EPSILON) &&
+           BETWEEN(q.z, c.z - l - EPSILON, c.z + l + EPSILON) &&
            (plane_is_transformed_point_on_surface(&s->p3, q) || plane_is_transformed_point_on_surface(&s->p4, q)))
     return 1;
   return 0;
@@ -581,6 +606,7 @@ static Camera camera_new(int width, int height, Vec center) {                   
   return c;
 }
 static Ray camera_create_ray(const Camera *c, double x, double y) {                 /* camera.rs:65-74 */
+  FL(7);
   double sx = ((x / (double)c->width) - 0.5) * c->aspect_ratio;
   double sy = ((double)c->height - 1.0 - y) / (double)c->height - 0.5;
   Ray r;
@@ -628,6 +654,7 @@ static void add_shadow(void *vctx, double d) {                                  
   ShadowCtx *c = (ShadowCtx *)vctx;
   if (d > EPSILON && d < c->distance) {
     CNT(C_SHADOW_HIT);
+    FL(1);
     c->transparency *= c->cached->material.transparency;   /* get_transparency_at_uv(uv): constant */
   }
 }
@@ -639,9 +666,11 @@ static Vec reflected_dir(Vec incident, Vec normal) {                            
 static Vec refracted_dir(Vec incident, Vec normal, double r, int *tir) {            /* raytracer.rs:336-353 */
   CNT(C_REFRACT_DIR);
   double cos_1 = v_dot(v_scale(incident, -1.0), normal);
+  FL(5);
   double v = 1.0 - r * r * (1.0 - cos_1 * cos_1);
   *tir = v < 0.0;
   if (*tir) return v_new(0.0, 0.0, 0.0);
+  FL(3);   /* sqrt, r * cos_1, - cos_2 */
   double cos_2 = sqrt(v);
   Vec result = v_add(v_scale(incident, r), v_scale(normal, r * cos_1 - cos_2));
   return v_normalized(result);
@@ -683,8 +712,8 @@ static Color get_ray_color(const orc_scene *sc, Ray ray, int depth) {           
     if (sh.transparency == 0.0) continue;                                           /* :200-202 */
     CNT(C_LIGHT_LIT);
     double angle = v_angle(shadow_ray.direction, normal);
-    if (angle >= PI / 2.0) angle = PI - angle;                                      /* :210-214 */
-    double intensity = (angle < (PI / 2.0) && angle >= 0.0) ? 1.0 - (angle / (PI / 2.0)) : 0.0;
+    if (angle >= PI / 2.0) { FL(1); angle = PI - angle; }                           /* :210-214 */
+    double intensity = (angle < (PI / 2.0) && angle >= 0.0) ? (FL(2), 1.0 - (angle / (PI / 2.0))) : 0.0;
     Color light_color = c_intensify(c_intensify(light->color, intensity), sh.transparency);
     final_light = c_add(final_light, c_mul(c, light_color));                        /* :227 */
   }
@@ -702,14 +731,16 @@ static Color get_ray_color(const orc_scene *sc, Ray ray, int depth) {           
   if (depth < sc->max_depth && transparency != 0.0) {                               /* :242-259 */
     Ray refracted;
     refracted.point = v_add(ray.point, v_scale(ray.direction, nearest_distance));
+    FL(1);
     refracted.direction = refracted_dir(ray.direction, normal, r1 / r2, &tir);
     if (!tir) {
       CNT(C_RAY_REFRACT); CNT(C_COMBINE);
       Color rc = get_ray_color(sc, refracted, depth + 1);
+      FL(1);
       final_light = c_add(c_intensify(final_light, 1.0 - transparency), c_intensify(rc, transparency));
     }
   }
-  if (tir) reflectivity = reflectivity + (1.0 - reflectivity) * transparency;       /* :261-265 */
+  if (tir) { FL(3); reflectivity = reflectivity + (1.0 - reflectivity) * transparency; } /* :261-265 */
 
   if (depth < sc->max_depth && reflectivity != 0.0 && (!inside_out || tir)) {       /* :267-280 */
     Ray reflected;
@@ -717,6 +748,7 @@ static Color get_ray_color(const orc_scene *sc, Ray ray, int depth) {           
     reflected.direction = reflected_dir(ray.direction, normal);
     CNT(C_RAY_REFLECT); CNT(C_COMBINE);
     Color rc = get_ray_color(sc, reflected, depth + 1);
+    FL(1);
     final_light = c_add(c_intensify(final_light, 1.0 - reflectivity), c_intensify(rc, reflectivity));
   }
   return final_light;

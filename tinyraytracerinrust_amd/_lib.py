@@ -74,6 +74,7 @@ SIGNATURES = {
     "rt_ctx_create": (_I, [_I, ctypes.POINTER(_P)]),
     "rt_ctx_upload": (_I, [_P, _P]),
     "rt_render_rows": (_I, [_P, _U32, _U32, ctypes.c_int32, _P, ctypes.c_size_t, _P]),
+    "rt_render_row_bands": (_I, [_P, _U32, _U32, _U32, _U32, ctypes.c_int32, _P, ctypes.c_size_t, _P]),
     "rt_render_rows_f64": (_I, [_P, _U32, _U32, ctypes.c_int32, _P, ctypes.c_size_t, _P]),
     "rt_render_points_f64": (_I, [_P, _P, ctypes.c_size_t, ctypes.c_int32, _P, _P]),
     "rt_ctx_last_kernel_ms": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),

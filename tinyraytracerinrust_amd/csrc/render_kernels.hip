@@ -435,20 +435,26 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
   *ro = ld3(cam.center);
 }
 
-// Rows [y0, y1) of the full frame.  Workgroup = 16x16 pixels, wave = 8x8.
+// Output rows r = 0 .. n_rows-1 of a band layout: r -> full-frame row
+//   y = y_first + (r / band_rows) * band_pitch + r % band_rows
+// (a contiguous tile [y0, y1) is one band; the cyclic multi-GPU layout deals bands of
+// band_rows rows with pitch world * band_rows).  Workgroup = 16x16 output pixels, wave = 8x8.
 template <bool REFR, bool F64>
-__global__ __launch_bounds__(256) void render_rows_kernel(RtDevScene S, int y0, int y1, int max_depth,
-                                                          uint8_t* __restrict__ out, size_t stride) {
+__global__ __launch_bounds__(256) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
+                                                          int n_rows, int max_depth, uint8_t* __restrict__ out,
+                                                          size_t stride) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tiles_x = (S.width + 15) >> 4;
   const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
   const int x = (bx << 4) + ((wave & 1) << 3) + (lane & 7);
-  const int y = y0 + (by << 4) + ((wave >> 1) << 3) + (lane >> 3);
-  if (x >= S.width || y >= y1) return;
+  const int r = (by << 4) + ((wave >> 1) << 3) + (lane >> 3);
+  if (x >= S.width || r >= n_rows) return;
+  const int y = y_first + (r / band_rows) * band_pitch + r % band_rows;
+  if (y >= S.height) return;
   V3 ro, rd;
   camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
   const Col c = trace<REFR>(S, ro, rd, max_depth);
-  uint8_t* row = out + (size_t)(y - y0) * stride;
+  uint8_t* row = out + (size_t)r * stride;
   if constexpr (F64) {
     double* o = (double*)row + (size_t)x * 4;
     o[0] = c.r; o[1] = c.g; o[2] = c.b; o[3] = 1.0;                        // alpha is 1 after any colour op
@@ -587,43 +593,62 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   return RT_OK;
 }
 
-static int launch_rows(rt_ctx* c, uint32_t y0, uint32_t y1, int32_t max_depth, void* out, size_t stride,
-                       void* stream, bool f64) {
+static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_t band_pitch, uint32_t n_bands,
+                        int32_t max_depth, void* out, size_t stride, void* stream, bool f64) {
   if (!c || !out) return fail(RT_ERR_INVALID, "null argument");
   if (!c->uploaded) return fail(RT_ERR_INVALID, "no scene uploaded to this context");
-  if (y0 > y1 || y1 > (uint32_t)c->dev.height) return fail(RT_ERR_INVALID, "bad row range [%u, %u) for height %d", y0, y1, c->dev.height);
+  if (band_rows == 0 || n_bands == 0) return RT_OK;
+  if (band_pitch < band_rows && n_bands > 1) return fail(RT_ERR_INVALID, "band pitch %u < band rows %u", band_pitch, band_rows);
+  if (y_first >= (uint32_t)c->dev.height) return fail(RT_ERR_INVALID, "first row %u >= height %d", y_first, c->dev.height);
+  const uint64_t n_rows64 = (uint64_t)band_rows * n_bands;
+  if (n_rows64 > (1u << 24)) return fail(RT_ERR_INVALID, "too many rows");
+  const uint32_t n_rows = (uint32_t)n_rows64;
   size_t row_bytes = (size_t)c->dev.width * (f64 ? 32 : 4);
   if (stride < row_bytes) return fail(RT_ERR_INVALID, "row stride %zu < %zu", stride, row_bytes);
   if (max_depth < 0) max_depth = c->max_depth;
   if (max_depth > RT_MAX_DEPTH_CAP) return fail(RT_ERR_UNSUPPORTED, "max_depth %d > %d", max_depth, RT_MAX_DEPTH_CAP);
-  if (y0 == y1) return RT_OK;
   RT_HIP(hipSetDevice(c->device));
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   const bool dev_out = is_device_ptr(out);
   uint8_t* target = (uint8_t*)out;
   size_t tstride = stride;
   if (!dev_out) {
-    int rc = ensure_scratch(c, row_bytes * (y1 - y0));
+    int rc = ensure_scratch(c, row_bytes * n_rows);
     if (rc) return rc;
     target = (uint8_t*)c->scratch;
     tstride = row_bytes;
   }
-  const int tiles_x = (c->dev.width + 15) / 16, tiles_y = (int)((y1 - y0 + 15) / 16);
+  const int tiles_x = (c->dev.width + 15) / 16, tiles_y = (int)((n_rows + 15) / 16);
   dim3 grid((unsigned)(tiles_x * tiles_y)), block(256);
+  const int a0 = (int)y_first, a1 = (int)band_rows, a2 = (int)band_pitch, a3 = (int)n_rows;
   RT_HIP(hipEventRecord(c->ev0, st));
   const bool refr = c->dev.any_transparent != 0;
-  if (refr && f64) hipLaunchKernelGGL((render_rows_kernel<true, true>), grid, block, 0, st, c->dev, (int)y0, (int)y1, max_depth, target, tstride);
-  else if (refr) hipLaunchKernelGGL((render_rows_kernel<true, false>), grid, block, 0, st, c->dev, (int)y0, (int)y1, max_depth, target, tstride);
-  else if (f64) hipLaunchKernelGGL((render_rows_kernel<false, true>), grid, block, 0, st, c->dev, (int)y0, (int)y1, max_depth, target, tstride);
-  else hipLaunchKernelGGL((render_rows_kernel<false, false>), grid, block, 0, st, c->dev, (int)y0, (int)y1, max_depth, target, tstride);
+  if (refr && f64) hipLaunchKernelGGL((render_rows_kernel<true, true>), grid, block, 0, st, c->dev, a0, a1, a2, a3, max_depth, target, tstride);
+  else if (refr) hipLaunchKernelGGL((render_rows_kernel<true, false>), grid, block, 0, st, c->dev, a0, a1, a2, a3, max_depth, target, tstride);
+  else if (f64) hipLaunchKernelGGL((render_rows_kernel<false, true>), grid, block, 0, st, c->dev, a0, a1, a2, a3, max_depth, target, tstride);
+  else hipLaunchKernelGGL((render_rows_kernel<false, false>), grid, block, 0, st, c->dev, a0, a1, a2, a3, max_depth, target, tstride);
   RT_HIP(hipGetLastError());
   RT_HIP(hipEventRecord(c->ev1, st));
   c->timed = true;
   if (!dev_out) {
-    RT_HIP(hipMemcpy2DAsync(out, stride, target, tstride, row_bytes, y1 - y0, hipMemcpyDeviceToHost, st));
+    RT_HIP(hipMemcpy2DAsync(out, stride, target, tstride, row_bytes, n_rows, hipMemcpyDeviceToHost, st));
     RT_HIP(hipStreamSynchronize(st));
   }
   return RT_OK;
+}
+
+static int launch_rows(rt_ctx* c, uint32_t y0, uint32_t y1, int32_t max_depth, void* out, size_t stride,
+                       void* stream, bool f64) {
+  if (!c || !out) return fail(RT_ERR_INVALID, "null argument");
+  if (!c->uploaded) return fail(RT_ERR_INVALID, "no scene uploaded to this context");
+  if (y0 > y1 || y1 > (uint32_t)c->dev.height) return fail(RT_ERR_INVALID, "bad row range [%u, %u) for height %d", y0, y1, c->dev.height);
+  if (y0 == y1) return RT_OK;
+  return launch_bands(c, y0, y1 - y0, y1 - y0, 1, max_depth, out, stride, stream, f64);
+}
+
+int rt_render_row_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_t band_pitch, uint32_t n_bands,
+                        int32_t max_depth, uint8_t* rgba8, size_t row_stride_bytes, void* stream) {
+  return launch_bands(c, y_first, band_rows, band_pitch, n_bands, max_depth, rgba8, row_stride_bytes, stream, false);
 }
 
 int rt_render_rows(rt_ctx* c, uint32_t y0, uint32_t y1, int32_t max_depth, uint8_t* rgba8,
