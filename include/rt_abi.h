@@ -12,7 +12,7 @@
  *   - every function returns RT_OK (0) or a negative rt_status; none aborts;
  *     rt_last_error() returns a thread-local message for the last failure;
  *   - no torch / HIP types in signatures: plain pointers, sizes and an opaque
- *     `void* stream` (a hipStream_t, NULL = the context's own stream);
+ *     `void* stream` (a hipStream_t; NULL = the device's default stream, as in HIP);
  *   - the library owns rt_scene / rt_ctx; the caller owns every output buffer;
  *   - an rt_scene is immutable once uploaded and may be shared by threads; an
  *     rt_ctx is used by one host thread at a time; distinct contexts may run
@@ -60,7 +60,7 @@ typedef struct rt_material {         /* SolidColorMaterial / TexturedMaterial (m
 } rt_material;
 
 typedef struct rt_scene rt_scene;    /* a RayTracer (raytracer.rs:21-35): objects, lights, camera */
-typedef struct rt_ctx rt_ctx;        /* per-device context: stream, device scene, scratch        */
+typedef struct rt_ctx rt_ctx;        /* per-device context: device scene, scratch, timing events */
 
 /* ---- library ---------------------------------------------------------------------------- */
 int rt_abi_version(void);
@@ -142,9 +142,10 @@ int rt_render_rows_f64(rt_ctx* ctx, uint32_t y0, uint32_t y1, int32_t max_depth,
  * antialiaser.rs:108-112): xy = n pairs of doubles, out = n x 4 doubles. Device or host. */
 int rt_render_points_f64(rt_ctx* ctx, const double* xy, size_t n, int32_t max_depth,
                          double* rgba_f64, void* stream);
-/* Milliseconds of the last render launch on this context (HIP events on its stream). */
+/* Milliseconds of the last render launch on this context (HIP events recorded on the launch's
+ * stream around the kernel). */
 int rt_ctx_last_kernel_ms(rt_ctx* ctx, float* ms);
-int rt_ctx_synchronize(rt_ctx* ctx);
+int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launch */
 void rt_ctx_free(rt_ctx* ctx);
 
 /* ---- output ----------------------------------------------------------------------------- */

@@ -479,7 +479,7 @@ __global__ __launch_bounds__(256) void render_points_kernel(RtDevScene S, const 
 // ====================================================================== device context
 struct rt_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;       // last stream launched on (NULL = the default stream)
   void* d_blob = nullptr;
   size_t blob_bytes = 0;
   RtDevScene dev;
@@ -546,8 +546,7 @@ int rt_ctx_create(int device, rt_ctx** out) {
   rt_ctx* c = new rt_ctx();
   c->device = device;
   memset(&c->dev, 0, sizeof c->dev);
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
     delete c;
     return fail(RT_ERR_DEVICE, "stream/event creation failed");
   }
@@ -608,7 +607,8 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   if (max_depth < 0) max_depth = c->max_depth;
   if (max_depth > RT_MAX_DEPTH_CAP) return fail(RT_ERR_UNSUPPORTED, "max_depth %d > %d", max_depth, RT_MAX_DEPTH_CAP);
   RT_HIP(hipSetDevice(c->device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t st = (hipStream_t)stream;   // NULL = the device's default stream
+  c->stream = st;
   const bool dev_out = is_device_ptr(out);
   uint8_t* target = (uint8_t*)out;
   size_t tstride = stride;
@@ -668,7 +668,8 @@ int rt_render_points_f64(rt_ctx* c, const double* xy, size_t n, int32_t max_dept
   if (max_depth > RT_MAX_DEPTH_CAP) return fail(RT_ERR_UNSUPPORTED, "max_depth %d > %d", max_depth, RT_MAX_DEPTH_CAP);
   if (n == 0) return RT_OK;
   RT_HIP(hipSetDevice(c->device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t st = (hipStream_t)stream;   // NULL = the device's default stream
+  c->stream = st;
   const bool dev_in = is_device_ptr(xy), dev_out = is_device_ptr(out);
   const double* in = xy;
   double* target = out;
@@ -711,12 +712,11 @@ int rt_ctx_synchronize(rt_ctx* c) {
 void rt_ctx_free(rt_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamSynchronize(c->stream);
   if (c->d_blob) (void)hipFree(c->d_blob);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 

@@ -171,8 +171,7 @@ class Renderer:
     def render_rows_into(self, y0: int, y1: int, out_ptr: int, row_stride: int, max_depth: int = -1,
                          stream: Optional[int] = None, f64: bool = False) -> None:
         fn = lib().rt_render_rows_f64 if f64 else lib().rt_render_rows
-        check(fn(self.h, y0, y1, max_depth, ctypes.c_void_p(out_ptr), row_stride,
-                 ctypes.c_void_p(stream) if stream else None))
+        check(fn(self.h, y0, y1, max_depth, ctypes.c_void_p(out_ptr), row_stride, ctypes.c_void_p(stream or 0)))
 
     def render_rows(self, y0: int, y1: int, max_depth: int = -1, f64: bool = False, out=None,
                     stream=None):
