@@ -10,7 +10,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librt_mi355x.so")
+# RT_LIB_PATH: load an alternative build (kernel-variant experiments, tools/); default in-tree.
+LIB_PATH = os.environ.get("RT_LIB_PATH") or os.path.join(HERE, "librt_mi355x.so")
 
 RT_OK = 0
 STATUS_NAMES = {

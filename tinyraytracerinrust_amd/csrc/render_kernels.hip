@@ -186,6 +186,30 @@ __device__ bool leaf_filter(const RtDevScene& S, const RtLeaf* L, V3 p) {
   return true;
 }
 
+// ------------------------------------------------------------------ conservative culling
+// Does the ray segment t in [0, tmax] come near the box?  Only ever answers "no" when no point of
+// the segment is inside [lo, hi]; boxes are inflated on the host (scene.cpp leaf_box) and tmax
+// carries a relative margin, so f64 rounding here cannot cull a hit the exact code would accept.
+// NaN anywhere makes the comparisons false and the answer "yes" (evaluate exactly).
+__device__ __forceinline__ bool box_may_hit(const double* lo, const double* hi, V3 o, V3 d, V3 inv, double tmax) {
+  double tn = 0.0, tf = tmax;
+#define RT_BOXAX(P, D, I, IV)                                                   \
+  if (D == 0.0) {                                                               \
+    if (P < lo[I] || P > hi[I]) return false;                                   \
+  } else {                                                                      \
+    double a = (lo[I] - P) * IV, b = (hi[I] - P) * IV;                          \
+    if (a > b) { double tmp = a; a = b; b = tmp; }                              \
+    if (a > tn) tn = a;                                                         \
+    if (b < tf) tf = b;                                                         \
+  }
+  RT_BOXAX(o.x, d.x, 0, inv.x)
+  RT_BOXAX(o.y, d.y, 1, inv.y)
+  RT_BOXAX(o.z, d.z, 2, inv.z)
+#undef RT_BOXAX
+  return !(tn > tf);
+}
+__device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) + 1e-7; }
+
 // ------------------------------------------------------------------ traversal (raytracer.rs)
 // Nearest hit over all objects in draw order: accept d if d > EPS && d < nearest
 // (raytracer.rs:141-150).  The acceptance test is pure, so it runs BEFORE the (pure) CSG
@@ -193,11 +217,18 @@ __device__ bool leaf_filter(const RtDevScene& S, const RtLeaf* L, V3 p) {
 __device__ int nearest_hit(const RtDevScene& S, V3 ro, V3 rd, double* dist) {
   double best = INFINITY;
   int bobj = -1;
+  const V3 inv = {1.0 / rd.x, 1.0 / rd.y, 1.0 / rd.z};
   for (int o = 0; o < S.n_objects; ++o) {
     const RtObject* O = &S.objects[o];
+    if (O->cull == RT_CULL_ALWAYS) continue;
+    if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, ro, rd, inv, cull_tmax(best))) continue;
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
     for (int l = lb; l < le; ++l) {
       const RtLeaf* L = &S.leaves[l];
+      if (O->leaf_cull) {
+        if (L->cull == RT_CULL_ALWAYS) continue;
+        if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, ro, rd, inv, cull_tmax(best))) continue;
+      }
       double t0 = 0.0, t1 = 0.0;
       int n = leaf_candidates(L, ro, rd, &t0, &t1);
       const bool filtered = L->prog_end != L->prog_begin;
@@ -218,13 +249,20 @@ __device__ int nearest_hit(const RtDevScene& S, V3 ro, V3 rd, double* dist) {
 // host), objects of transparency exactly 1.0 are skipped (x * 1.0 == x).
 __device__ double shadow_transparency(const RtDevScene& S, V3 p, V3 dir, double dist) {
   double tr = 1.0;
+  const V3 inv = {1.0 / dir.x, 1.0 / dir.y, 1.0 / dir.z};
+  const double tmax = cull_tmax(dist);
   for (int o = 0; o < S.n_objects; ++o) {
     const RtObject* O = &S.objects[o];
-    if (O->shadow_skip) continue;
+    if (O->shadow_skip || O->cull == RT_CULL_ALWAYS) continue;
+    if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, p, dir, inv, tmax)) continue;
     const double tobj = O->transparency;
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
     for (int l = lb; l < le; ++l) {
       const RtLeaf* L = &S.leaves[l];
+      if (O->leaf_cull) {
+        if (L->cull == RT_CULL_ALWAYS) continue;
+        if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, p, dir, inv, tmax)) continue;
+      }
       double t0 = 0.0, t1 = 0.0;
       int n = leaf_candidates(L, p, dir, &t0, &t1);
       const bool filtered = L->prog_end != L->prog_begin;
@@ -439,8 +477,11 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
 //   y = y_first + (r / band_rows) * band_pitch + r % band_rows
 // (a contiguous tile [y0, y1) is one band; the cyclic multi-GPU layout deals bands of
 // band_rows rows with pitch world * band_rows).  Workgroup = 16x16 output pixels, wave = 8x8.
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU 4   // 128 VGPRs: measured best (profiles/r01_occupancy_sweep.txt)
+#endif
 template <bool REFR, bool F64>
-__global__ __launch_bounds__(256) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU))) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
                                                           int n_rows, int max_depth, uint8_t* __restrict__ out,
                                                           size_t stride) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

@@ -27,6 +27,15 @@ enum RtNodeKind : int32_t {
   RT_N_UNION = 3, RT_N_INTERSECTION = 4, RT_N_DIFFERENCE = 5
 };
 
+// Conservative culling bounds (world-space AABB of every point where an ACCEPTED hit of the
+// leaf / object can lie, inflated far beyond f64 rounding).  They only skip work whose result
+// cannot be used: the rendered bits are unchanged (DESIGN.md "Culling").
+enum RtCull : int32_t {
+  RT_CULL_NONE = 0,     // unbounded (planes, singular transforms): always evaluate
+  RT_CULL_BOX = 1,      // test the ray segment against [blo, bhi]
+  RT_CULL_ALWAYS = 2,   // provably no accepted hit (empty CSG intersection)
+};
+
 // Hit-filter program opcodes (postfix over a bit stack).
 enum RtProgOp : int32_t {
   RT_OP_INSIDE = 0,     // push leaf[arg].is_inside(p)
@@ -54,10 +63,11 @@ struct alignas(16) RtLeaf {
   double pl[6][4];      // plane leaf: pl[0] = raw (a,b,c,d); cube: p1..p6 raw (a,b,c,d)
   double pn[6][3];      // matching transformed unit normals (MathPlane::normal)
   double pnorm[3];      // plane leaf: Vector::new(a,b,c).normalized() (math_shapes.rs:169)
+  double blo[3], bhi[3];// culling box of this leaf's accepted hits (own bound ^ required-inside siblings)
   int32_t kind;         // RtNodeKind (leaf kinds only)
   int32_t prog_begin;   // hit-filter program [prog_begin, prog_end)
   int32_t prog_end;
-  int32_t pad;
+  int32_t cull;         // RtCull
 };
 
 struct RtNode {
@@ -72,9 +82,12 @@ struct alignas(16) RtObject {
   int32_t textured;                 // 0 solid, 1 texture
   int32_t tex;                      // texture index
   int32_t shadow_skip;              // transparency == 1.0: shadow multiplies by 1 -> no-op
-  int32_t pad;
+  int32_t cull;                     // RtCull for the object box (hull of its leaves' boxes)
   double color[3];                  // material colour (solid)
   double reflectivity, transparency;
+  double blo[3], bhi[3];
+  int32_t leaf_cull;                // 1: per-leaf boxes are tighter than the object box
+  int32_t pad2;
 };
 
 struct RtTexture {

@@ -5,6 +5,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -181,12 +182,85 @@ static int make_leaf(const ShapeRec& s, RtLeaf* L) {
   return RT_OK;
 }
 
+// ---------------------------------------------------------------- culling bounds
+// World-space AABB of the region {p : Minv * p in B} for an object-space ball / box B.  The
+// reference tests points through the INVERSE matrix (which for multi-axis rotations is not the
+// exact inverse of the forward matrix, transformation.rs:149-159), so the region is the image of
+// B under Minv^-1, computed here in long double and inflated generously.
+struct Box { double lo[3], hi[3]; int kind; };   // kind: RtCull
+
+static Box box_infinite() { Box b; for (int i = 0; i < 3; ++i) { b.lo[i] = -INFINITY; b.hi[i] = INFINITY; } b.kind = RT_CULL_NONE; return b; }
+static Box box_empty() { Box b; for (int i = 0; i < 3; ++i) { b.lo[i] = INFINITY; b.hi[i] = -INFINITY; } b.kind = RT_CULL_ALWAYS; return b; }
+
+static Box box_hull(const Box& a, const Box& b) {
+  if (a.kind == RT_CULL_ALWAYS) return b;
+  if (b.kind == RT_CULL_ALWAYS) return a;
+  if (a.kind == RT_CULL_NONE || b.kind == RT_CULL_NONE) return box_infinite();
+  Box r;
+  r.kind = RT_CULL_BOX;
+  for (int i = 0; i < 3; ++i) { r.lo[i] = fmin(a.lo[i], b.lo[i]); r.hi[i] = fmax(a.hi[i], b.hi[i]); }
+  return r;
+}
+static Box box_meet(const Box& a, const Box& b) {
+  if (a.kind == RT_CULL_ALWAYS || b.kind == RT_CULL_ALWAYS) return box_empty();
+  if (a.kind == RT_CULL_NONE) return b;
+  if (b.kind == RT_CULL_NONE) return a;
+  Box r;
+  r.kind = RT_CULL_BOX;
+  for (int i = 0; i < 3; ++i) {
+    r.lo[i] = fmax(a.lo[i], b.lo[i]);
+    r.hi[i] = fmin(a.hi[i], b.hi[i]);
+    if (r.lo[i] > r.hi[i]) return box_empty();
+  }
+  return r;
+}
+
+// Leaf's own region (points its hits and its is_inside can involve), in world space.
+static Box leaf_box(const ShapeRec& s) {
+  if (s.kind == SHAPE_PLANE) return box_infinite();
+  const double* iv = s.t.inverse;
+  long double A[3][3], b[3], Ai[3][3];
+  for (int i = 0; i < 3; ++i) { for (int j = 0; j < 3; ++j) A[i][j] = iv[4 * i + j]; b[i] = iv[4 * i + 3]; }
+  long double det = A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) - A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
+                    A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
+  if (!(fabsl(det) > 1e-300L) || !isfinite((double)det)) return box_infinite();
+  Ai[0][0] = (A[1][1] * A[2][2] - A[1][2] * A[2][1]) / det;
+  Ai[0][1] = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) / det;
+  Ai[0][2] = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) / det;
+  Ai[1][0] = (A[1][2] * A[2][0] - A[1][0] * A[2][2]) / det;
+  Ai[1][1] = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) / det;
+  Ai[1][2] = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) / det;
+  Ai[2][0] = (A[1][0] * A[2][1] - A[1][1] * A[2][0]) / det;
+  Ai[2][1] = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
+  Ai[2][2] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
+  const long double eps = RT_EPSILON;
+  long double c[3], half[3];
+  for (int i = 0; i < 3; ++i) c[i] = (long double)s.center[i] - b[i];
+  Box r;
+  r.kind = RT_CULL_BOX;
+  for (int i = 0; i < 3; ++i) {
+    long double wc = Ai[i][0] * c[0] + Ai[i][1] * c[1] + Ai[i][2] * c[2];
+    if (s.kind == SHAPE_SPHERE) {                 // ball of radius r (+EPS: is_inside's slack)
+      long double rad = fabsl((long double)s.size) + eps;
+      half[i] = rad * sqrtl(Ai[i][0] * Ai[i][0] + Ai[i][1] * Ai[i][1] + Ai[i][2] * Ai[i][2]);
+    } else {                                      // box of half-length size/2 (+EPS)
+      long double h = fabsl((long double)s.size / 2.0L) + eps;
+      half[i] = h * (fabsl(Ai[i][0]) + fabsl(Ai[i][1]) + fabsl(Ai[i][2]));
+    }
+    long double margin = 1e-6L * (fabsl(wc) + half[i]) + 1e-6L;
+    r.lo[i] = (double)(wc - half[i] - margin);
+    r.hi[i] = (double)(wc + half[i] + margin);
+    if (!isfinite(r.lo[i]) || !isfinite(r.hi[i])) return box_infinite();
+  }
+  return r;
+}
+
 struct Flattener {
   const rt_scene& s;
   FlatScene& f;
   int32_t node_begin = 0;
-  std::vector<int32_t> leaf_node;      // per leaf (object-relative): node index
   std::vector<int32_t> parent;         // per node (object-relative): parent node or -1
+  std::vector<Box> box;                // per node (object-relative): region of its is_inside / hits
   int depth_guard = 0;
 
   // Emit the subtree of shape id `sid`; returns its object-relative node index.
@@ -215,7 +289,14 @@ struct Flattener {
     int32_t idx = (int32_t)f.nodes.size() - node_begin;
     f.nodes.push_back(n);
     parent.push_back(-1);
-    if (n.kind >= RT_N_UNION) { parent[n.a] = idx; parent[n.b] = idx; }
+    if (n.kind >= RT_N_UNION) {
+      parent[n.a] = idx; parent[n.b] = idx;
+      // csg.rs:126-135: union -> either child, intersection -> both, difference -> inside a
+      box.push_back(n.kind == RT_N_UNION ? box_hull(box[n.a], box[n.b])
+                    : n.kind == RT_N_INTERSECTION ? box_meet(box[n.a], box[n.b]) : box[n.a]);
+    } else {
+      box.push_back(leaf_box(r));
+    }
     return idx;
   }
 
@@ -253,11 +334,13 @@ int flatten(const rt_scene& s, FlatScene* out) {
     if (ob.node_count > 32) return fail(RT_ERR_UNSUPPORTED, "object with %d CSG nodes (max 32)", ob.node_count);
     // Hit-filter program per leaf: for every CSG ancestor, the sibling's is_inside test with
     // the polarity of csg.rs:43-95 (Union: !in, !in; Intersection: in, in; Difference: !in, in).
+    Box obox = box_empty();
+    int n_leaf_boxes_tighter = 0;
     for (int32_t ni = 0; ni < ob.node_count; ++ni) {
       const RtNode& n = f.nodes[ob.node_begin + ni];
       if (n.kind >= RT_N_UNION) continue;
-      RtLeaf& L = f.leaves[n.leaf];
-      L.prog_begin = (int32_t)f.prog.size();
+      f.leaves[n.leaf].prog_begin = (int32_t)f.prog.size();
+      Box useful = fl.box[ni];             // an accepted hit of this leaf lies on the leaf ...
       int32_t child = ni, par = fl.parent[ni];
       while (par >= 0) {
         const RtNode& P = f.nodes[ob.node_begin + par];
@@ -266,12 +349,20 @@ int flatten(const rt_scene& s, FlatScene* out) {
         int want = P.kind == RT_N_INTERSECTION ? 1 : P.kind == RT_N_UNION ? 0 : (is_a ? 0 : 1);
         fl.emit_inside(sib);
         f.prog.push_back({RT_OP_REQUIRE, want});
+        if (want) useful = box_meet(useful, fl.box[sib]);   // ... and inside every required sibling
         child = par;
         par = fl.parent[par];
       }
-      f.leaves[n.leaf].prog_end = (int32_t)f.prog.size();
-      (void)L;
+      RtLeaf& L = f.leaves[n.leaf];
+      L.prog_end = (int32_t)f.prog.size();
+      L.cull = useful.kind;
+      for (int i = 0; i < 3; ++i) { L.blo[i] = useful.lo[i]; L.bhi[i] = useful.hi[i]; }
+      obox = box_hull(obox, useful);
+      if (useful.kind != RT_CULL_NONE) ++n_leaf_boxes_tighter;
     }
+    ob.cull = obox.kind;
+    for (int i = 0; i < 3; ++i) { ob.blo[i] = obox.lo[i]; ob.bhi[i] = obox.hi[i]; }
+    ob.leaf_cull = ob.leaf_count > 1 && n_leaf_boxes_tighter > 0;
     const rt_material& m = o.mat;
     ob.textured = m.texture >= 0;
     ob.tex = m.texture >= 0 ? m.texture : 0;
@@ -297,6 +388,18 @@ int flatten(const rt_scene& s, FlatScene* out) {
     f.texels.insert(f.texels.end(), t.rgba.begin(), t.rgba.end());
     off += (int64_t)t.rgba.size();
     while (off % 16) { f.texels.push_back(0); ++off; }
+  }
+  if (getenv("RT_DUMP_FLAT")) {                                // debugging aid: culling boxes
+    for (size_t o = 0; o < f.objects.size(); ++o) {
+      const RtObject& ob = f.objects[o];
+      fprintf(stderr, "object %zu cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] leaves %d leaf_cull=%d\n", o, ob.cull,
+              ob.blo[0], ob.blo[1], ob.blo[2], ob.bhi[0], ob.bhi[1], ob.bhi[2], ob.leaf_count, ob.leaf_cull);
+      for (int l = ob.leaf_begin; l < ob.leaf_begin + ob.leaf_count; ++l) {
+        const RtLeaf& L = f.leaves[l];
+        fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d\n", l, L.kind, L.cull,
+                L.blo[0], L.blo[1], L.blo[2], L.bhi[0], L.bhi[1], L.bhi[2], L.prog_end - L.prog_begin);
+      }
+    }
   }
   // PerspectiveCamera::new(width, height, center, None, None, None) (camera.rs:30-54)
   V center = {s.cam_center[0], s.cam_center[1], s.cam_center[2]};
