@@ -111,6 +111,11 @@ int rt_scene_compile(const char* scene_text, const char* asset_dir, double time,
                      uint32_t width, uint32_t height, rt_scene** out);
 int rt_scene_info(const rt_scene* scene, int32_t* n_objects, int32_t* n_lights, int32_t* n_leaves,
                   uint32_t* width, uint32_t* height);
+/* Introspection (tests, debuggers): the camera as PerspectiveCamera::new builds it
+ * (camera.rs:30-54): out = center[3], direction[3], right[3], up[3], aspect_ratio. */
+int rt_scene_get_camera(const rt_scene* scene, double out[13]);
+/* Light i: point[3] (world space, as stored by add_light) and color[4]. */
+int rt_scene_get_light(const rt_scene* scene, int32_t i, double point[3], double color[4]);
 void rt_scene_free(rt_scene* scene);
 
 /* ---- device rendering (replaces RayTracer::get_pixel + DebugWindow::render_lines) ------ */

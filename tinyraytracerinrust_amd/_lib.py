@@ -70,6 +70,8 @@ SIGNATURES = {
     "rt_scene_info": (_I, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_U32),
                            ctypes.POINTER(_U32)]),
+    "rt_scene_get_camera": (_I, [_P, _D3]),
+    "rt_scene_get_light": (_I, [_P, ctypes.c_int32, _D3, _D3]),
     "rt_scene_free": (None, [_P]),
     "rt_device_count": (_I, [ctypes.POINTER(_I)]),
     "rt_ctx_create": (_I, [_I, ctypes.POINTER(_P)]),

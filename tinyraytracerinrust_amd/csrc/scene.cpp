@@ -573,6 +573,27 @@ int rt_scene_info(const rt_scene* s, int32_t* n_objects, int32_t* n_lights, int3
   if (height) *height = s->height;
   return RT_OK;
 }
+int rt_scene_get_camera(const rt_scene* s, double out[13]) {
+  if (!s || !out) return fail(RT_ERR_INVALID, "null argument");
+  FlatScene f;
+  rt_scene tmp;                                       // camera only: no need to flatten objects
+  tmp.width = s->width; tmp.height = s->height;
+  memcpy(tmp.cam_center, s->cam_center, sizeof tmp.cam_center);
+  int rc = flatten(tmp, &f);
+  if (rc) return rc;
+  for (int i = 0; i < 3; ++i) {
+    out[i] = f.cam.center[i]; out[3 + i] = f.cam.direction[i]; out[6 + i] = f.cam.right[i]; out[9 + i] = f.cam.up[i];
+  }
+  out[12] = f.cam.aspect;
+  return RT_OK;
+}
+int rt_scene_get_light(const rt_scene* s, int32_t i, double point[3], double color[4]) {
+  if (!s || !point || !color) return fail(RT_ERR_INVALID, "null argument");
+  if (i < 0 || i >= (int32_t)s->lights.size()) return fail(RT_ERR_INVALID, "light %d out of range", i);
+  memcpy(point, s->lights[i].p, sizeof s->lights[i].p);
+  memcpy(color, s->lights[i].color, sizeof s->lights[i].color);
+  return RT_OK;
+}
 void rt_scene_free(rt_scene* s) { delete s; }
 
 int rt_scene_compile(const char* text, const char* asset_dir, double time, uint32_t width,

@@ -142,6 +142,17 @@ class Scene:
         return {"objects": no.value, "lights": nl.value, "leaves": nlf.value,
                 "width": w.value, "height": h.value}
 
+    def camera(self) -> dict:
+        out = (ctypes.c_double * 13)()
+        check(lib().rt_scene_get_camera(self.h, out))
+        v = list(out)
+        return {"center": v[0:3], "direction": v[3:6], "right": v[6:9], "up": v[9:12], "aspect": v[12]}
+
+    def light(self, i: int) -> Tuple[list, list]:
+        p, c = (ctypes.c_double * 3)(), (ctypes.c_double * 4)()
+        check(lib().rt_scene_get_light(self.h, i, p, c))
+        return list(p), list(c)
+
     def free(self) -> None:
         if self.h and self.h.value:
             lib().rt_scene_free(self.h)
