@@ -6,10 +6,12 @@ globes.scene at t=0, 3840x2160, max_depth 10 (the reference's hard-coded depth,
 raytracer.rs:65), default test light, RGBA8 output.  One step = one frame:
 
 * N = 1: one kernel launch renders all 2160 rows into an HBM framebuffer;
-* N > 1: one process per GPU (torchrun); rank r renders its row tile (contiguous by default,
-  ``--layout cyclic`` deals 16-row bands round-robin) and one RCCL all_gather_into_tensor over
-  xGMI assembles the frame on every rank (cyclic adds a local reorder).  Total work is fixed as
-  N grows: scaling "strong".
+* N > 1: one process per GPU (torchrun); rank r renders its rows -- 8-row bands dealt
+  round-robin (``--layout cyclic``, default: balances cheap sky rows against floor rows with
+  reflection chains; ``contiguous`` = one tile per rank) -- and one RCCL all_gather_into_tensor
+  over xGMI assembles the frame on every rank, followed by one local permute copy for the cyclic
+  layout.  Frame k's gather overlaps frame k+1's render (double-buffered; ``--no-overlap``
+  serialises).  Total work is fixed as N grows: scaling "strong".
 
 value = W*H primary rays per frame * K frames / (max over ranks of the timed wall time), in
 millions.  The scene blob and texture are uploaded before the timed region (inputs resident in
@@ -54,8 +56,13 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="globes4k", choices=sorted(CONFIGS))
-    ap.add_argument("--layout", default="contiguous", choices=["contiguous", "cyclic"])
-    ap.add_argument("--band", type=int, default=16)
+    ap.add_argument("--layout", default="cyclic", choices=["contiguous", "cyclic"],
+                    help="row tiling for N > 1 (cyclic 8-row bands balance sky vs floor rows)")
+    ap.add_argument("--band", type=int, default=8)
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N > 1: do not overlap frame k's all-gather with frame k+1's render")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="exercise the N > 1 path (process group, bands, all-gather) even at N = 1")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--png", default="", help="write the rendered frame (rank 0) to this PNG")
@@ -127,7 +134,8 @@ def main():
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    multi = world > 1 or a.force_collective
+    if multi:
         dist.init_process_group("nccl", device_id=dev)
 
     scene, W, H, t, depth = CONFIGS[a.config]
@@ -136,48 +144,68 @@ def main():
     rt.load_scene(text, t, asset_dir=SCENES)
     rend = rt.renderer                                    # uploads the scene blob + texture
 
-    layout = a.layout if world > 1 else "contiguous"
+    layout = a.layout if multi else "contiguous"
     band = a.band if layout == "cyclic" else -(-H // world)
     slot_rows = D.rows_per_rank(H, world, layout, band)
     mine = owned_rows(H, world, rank, layout, band)
-    n_bands = len(mine)
-    if layout == "contiguous":
-        y_first, band_rows, pitch = mine[0][0], mine[0][1] - mine[0][0], H
-    else:
-        y_first, band_rows, pitch = mine[0][0], band, world * band
-    frame = torch.zeros((max(H, world * slot_rows), W, 4), dtype=torch.uint8, device=dev)
-    slot = frame if world == 1 else torch.zeros((slot_rows, W, 4), dtype=torch.uint8, device=dev)
+    y_first, band_rows, pitch, n_bands = D.band_params(H, world, rank, layout, band)
+    frame = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
+    overlap = multi and not a.no_overlap
+    # N > 1: double-buffered slot / gather buffers so frame k's all-gather (RCCL stream) runs
+    # under frame k+1's render (compute stream); every frame is still fully assembled.
+    nbuf = 2 if overlap else 1
+    slots = [torch.zeros((slot_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
+    gath = [torch.zeros((world * slot_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
+    frames = [frame] + [torch.zeros_like(frame) for _ in range(nbuf - 1)]
+    pending = [None]           # (work, buffer index) of the gather not yet assembled
 
-    def step(ev0=None, ev1=None):
+    def finish(p):
+        work, b = p
+        work.wait()
+        D.assemble(gath[b], H, world, layout, band, out=frames[b])
+
+    def step(i, ev0=None, ev1=None):
+        b = i % nbuf
         if ev0 is not None:
             ev0.record(stream)
-        if world == 1:
+        if not multi:
             rend.render_rows(0, H, max_depth=depth, out=frame, stream=stream)
         else:
-            rend.render_row_bands(y_first, band_rows, pitch, n_bands, slot, max_depth=depth, stream=stream)
+            rend.render_row_bands(y_first, band_rows, pitch, n_bands, slots[b], max_depth=depth, stream=stream)
         if ev1 is not None:
             ev1.record(stream)
-        if world > 1:
-            dist.all_gather_into_tensor(frame, slot)
-            if layout == "cyclic":
-                D.assemble(frame, H, world, layout, band)
+        if multi:
+            work = dist.all_gather_into_tensor(gath[b], slots[b], async_op=True)
+            if pending[0] is not None:
+                finish(pending[0])
+            pending[0] = (work, b)
+            if not overlap:
+                finish(pending[0])
+                pending[0] = None
 
-    for _ in range(a.warmup):
-        step()
+    def drain():
+        if pending[0] is not None:
+            finish(pending[0])
+            pending[0] = None
+
+    for i in range(a.warmup):
+        step(i)
+    drain()
     torch.cuda.synchronize(dev)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step(*evs[i])
+        step(a.warmup + i, *evs[i])
+    drain()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if multi:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if multi:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
@@ -185,10 +213,10 @@ def main():
     mean_kernel_ms = sum(kernel_ms) / len(kernel_ms)
 
     if rank == 0 and a.png:
-        T.write_png(a.png, frame[:H].cpu().numpy())
+        T.write_png(a.png, frames[(a.warmup + a.steps - 1) % nbuf].cpu().numpy())
 
     if rank != 0:
-        if world > 1:
+        if multi:
             dist.destroy_process_group()
         return
 
@@ -215,7 +243,8 @@ def main():
         "config": {
             "workload": f"{scene}.scene {W}x{H} t={t:g} max_depth {depth}, one frame per step",
             "scene": f"{scene}.scene", "width": W, "height": H, "time": t, "max_depth": depth,
-            "parallelism": f"rowtile{world}" + ("" if world == 1 else f"-{layout}"),
+            "parallelism": f"rowtile{world}" + ("" if not multi else f"-{layout}" + (f"{band}" if layout == "cyclic" else "")),
+            "collective": None if not multi else "all_gather_into_tensor (RCCL)" + (", overlapped with next frame" if overlap else ""),
             "frame_bytes": W * H * 4,
         },
         "roofline": {
@@ -243,12 +272,12 @@ def main():
         },
         "cpu_baseline": None,
     }
-    if world == 1 and not a.no_cpu_baseline:
+    if world == 1 and not multi and not a.no_cpu_baseline:
         cb = cpu_baseline(text, W, H, t, depth, a.cpu_threads)
         cb["gpu_over_cpu"] = round(line["value"] / cb["value"], 1)
         line["cpu_baseline"] = cb
     print(json.dumps(line), flush=True)
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 

@@ -164,3 +164,26 @@ def test_4k_globes_sampled_rows(T, worldmap):
     assert_close(got, None, ref_u8, None, "4K globes sampled rows")
     again = rt.renderer.render_rows(0, H).cpu().numpy()
     assert np.array_equal(frame, again)
+
+
+@pytest.mark.parametrize("world,layout,band", [(2, "contiguous", 0), (3, "cyclic", 8), (8, "cyclic", 8),
+                                               (8, "contiguous", 0), (5, "cyclic", 16)])
+def test_row_bands_assemble_like_ranks(T, world, layout, band):
+    """What each rank of the multi-GPU path does (rt_render_row_bands into its slot of the
+    gather buffer) followed by the assembly, simulated on one GPU: equals the plain frame."""
+    import torch
+    from tinyraytracerinrust_amd import distributed as D
+    W, H = 200, 150
+    rt = T.RayTracer(W, H)
+    rt.load_scene(scene_text("globes"), 0.0, asset_dir=SCENES)
+    r = rt.renderer
+    full = r.render_rows_host(0, H)
+    band = band or -(-H // world)
+    slot_rows = D.rows_per_rank(H, world, layout, band)
+    gath = torch.zeros((world * slot_rows, W, 4), dtype=torch.uint8, device="cuda")
+    for rank in range(world):
+        y_first, band_rows, pitch, n_bands = D.band_params(H, world, rank, layout, band)
+        r.render_row_bands(y_first, band_rows, pitch, n_bands, gath[rank * slot_rows:(rank + 1) * slot_rows])
+    frame = D.assemble(gath, H, world, layout, band)
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy(), full)

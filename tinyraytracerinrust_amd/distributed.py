@@ -47,6 +47,16 @@ def owned_rows(height: int, world: int, rank: int, layout: str = "contiguous", b
     return contiguous_rows(height, world, rank) if layout == "contiguous" else cyclic_rows(height, world, rank, band)
 
 
+def band_params(height: int, world: int, rank: int, layout: str, band: int) -> Tuple[int, int, int, int]:
+    """(y_first, band_rows, band_pitch, n_bands) of this rank's rows for rt_render_row_bands."""
+    own = owned_rows(height, world, rank, layout, band)
+    if not own:
+        return 0, 0, 0, 0
+    if layout == "contiguous":
+        return own[0][0], own[0][1] - own[0][0], height, 1
+    return own[0][0], band, world * band, len(own)
+
+
 def render_local(render_rows: Callable[[int, int, torch.Tensor], None], height: int, width: int, world: int,
                  rank: int, layout: str, band: int, device, dtype=torch.uint8) -> torch.Tensor:
     """This rank's slot: its rows packed densely (padding rows left zero)."""
@@ -58,18 +68,27 @@ def render_local(render_rows: Callable[[int, int, torch.Tensor], None], height: 
     return slot
 
 
-def assemble(gathered: torch.Tensor, height: int, world: int, layout: str, band: int) -> torch.Tensor:
-    """gathered: (world * slot_rows, W, 4) in rank order -> (H, W, 4) frame."""
+def assemble(gathered: torch.Tensor, height: int, world: int, layout: str, band: int,
+             out: torch.Tensor = None) -> torch.Tensor:
+    """gathered: (world * slot_rows, W, 4) in rank order -> (H, W, 4) frame.
+
+    Contiguous tiles are already in frame order (a view).  Cyclic slots hold bands
+    g = b * world + rank at slot rows [b * band, (b + 1) * band), so the frame is ONE permuted
+    copy: view (world, bands_per_rank, band, ...) -> swap the first two axes -> first H rows."""
     slot_rows = gathered.shape[0] // world
     if layout == "contiguous":
-        return gathered[:height]
-    frame = torch.empty((height,) + tuple(gathered.shape[1:]), dtype=gathered.dtype, device=gathered.device)
-    for rank in range(world):
-        r = rank * slot_rows
-        for y0, y1 in cyclic_rows(height, world, rank, band):
-            frame[y0:y1] = gathered[r:r + (y1 - y0)]
-            r += y1 - y0
-    return frame
+        frame = gathered[:height]
+        if out is not None:
+            out.copy_(frame)
+            return out
+        return frame
+    nbpr = slot_rows // band
+    tail = tuple(gathered.shape[1:])
+    perm = gathered.view((world, nbpr, band) + tail).transpose(0, 1).reshape((world * nbpr * band,) + tail)
+    if out is None:
+        return perm[:height].contiguous()
+    out.copy_(perm[:height])
+    return out
 
 
 def render_frame_distributed(render_rows: Callable[[int, int, torch.Tensor], None], height: int, width: int,

@@ -13,6 +13,8 @@ run timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/${TAG}_pytest_g
 tail -3 $OUT/${TAG}_pytest_gpu.txt
 run timeout -k 10 300 python bench.py --steps $STEPS --warmup 10 > $OUT/${TAG}_bench.json 2> $OUT/${TAG}_bench.err || { cat $OUT/${TAG}_bench.err | tail; exit 1; }
 cat $OUT/${TAG}_bench.json
+run timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 20 --warmup 5 --force-collective > $OUT/${TAG}_bench_collective.json 2> $OUT/${TAG}_bench_collective.err || { tail -20 $OUT/${TAG}_bench_collective.err; exit 1; }
+cat $OUT/${TAG}_bench_collective.json
 run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_kt -o run -- python3 bench.py --steps $STEPS --warmup 10 --no-cpu-baseline > $OUT/${TAG}_bench_kt.json 2> $OUT/${TAG}_kt.err || { tail $OUT/${TAG}_kt.err; exit 1; }
 [ "${PMC_PASSES:-1}" = "1" ] || { echo done; exit 0; }
 run timeout -k 10 120 rocprofv3 -L > $OUT/${TAG}_counters.txt 2>&1 || true
