@@ -121,6 +121,10 @@ def cpu_baseline(text, W, H, t, depth, threads):
 
 def main():
     a = parse()
+    # Exactly one JSON line on stdout: libraries (RCCL prints a version banner at communicator
+    # creation) write to fd 1 as well, so route fd 1 to stderr and keep a private copy for the line.
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
     import tinyraytracerinrust_amd as T
@@ -276,7 +280,8 @@ def main():
         cb = cpu_baseline(text, W, H, t, depth, a.cpu_threads)
         cb["gpu_over_cpu"] = round(line["value"] / cb["value"], 1)
         line["cpu_baseline"] = cb
-    print(json.dumps(line), flush=True)
+    json_out.write(json.dumps(line) + "\n")
+    json_out.flush()
     if multi:
         dist.destroy_process_group()
 

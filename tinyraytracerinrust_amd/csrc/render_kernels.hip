@@ -27,7 +27,26 @@
 
 namespace {
 
+// Scene tables are read-only for the whole launch: view them through the CONSTANT address space
+// (4) so uniform-index reads compile to scalar (SMEM) loads instead of per-lane VMEM loads.
+#define CAS __attribute__((address_space(4)))
+template <class T> using cptr = const CAS T*;
+template <class T> __device__ __forceinline__ cptr<T> as_const(const T* p) { return (cptr<T>)p; }
+
+struct DS {                         // device view of RtDevScene
+  cptr<RtObject> objects;
+  cptr<RtNode> nodes;
+  cptr<RtLeaf> leaves;
+  cptr<RtProg> prog;
+  cptr<RtLight> lights;
+  cptr<RtTexture> textures;
+  const uint8_t* texels;            // per-lane texel gathers stay global (vector) loads
+  int n_objects, n_lights;
+  int shadow_early_out;
+};
+
 constexpr double EPS = RT_EPSILON;
+#define RT_LIGHT_GROUP 4            // shadow transparencies held in registers per light group
 constexpr double PI_D = 3.14159265358979323846;   // std::f64::consts::PI
 
 struct V3 { double x, y, z; };
@@ -39,9 +58,9 @@ __device__ __forceinline__ V3 scale(V3 a, double s) { return {a.x * s, a.y * s, 
 __device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 __device__ __forceinline__ double len(V3 a) { return sqrt(dot(a, a)); }
 __device__ __forceinline__ V3 normalized(V3 a) { return scale(a, 1.0 / len(a)); }
-__device__ __forceinline__ V3 ld3(const double* p) { return {p[0], p[1], p[2]}; }
+template <class P> __device__ __forceinline__ V3 ld3(P p) { return {p[0], p[1], p[2]}; }
 // transform_vector (transformation.rs:53-59) with rows m[0..3], m[4..7], m[8..11]
-__device__ __forceinline__ V3 xf(const double* m, V3 v) {
+template <class P> __device__ __forceinline__ V3 xf(P m, V3 v) {
   return {m[0] * v.x + m[1] * v.y + m[2] * v.z + m[3],
           m[4] * v.x + m[5] * v.y + m[6] * v.z + m[7],
           m[8] * v.x + m[9] * v.y + m[10] * v.z + m[11]};
@@ -61,11 +80,11 @@ __device__ __forceinline__ uint32_t to_u8(double c) {
 }
 
 // ------------------------------------------------------------------ primitives (math_shapes.rs)
-__device__ __forceinline__ bool on_plane(const double* pl, V3 q) {        // :162-164
+template <class P> __device__ __forceinline__ bool on_plane(P pl, V3 q) {        // :162-164
   return fabs(pl[0] * q.x + pl[1] * q.y + pl[2] * q.z + pl[3]) < EPS;
 }
 
-__device__ bool leaf_inside(const RtLeaf* L, V3 p) {
+__device__ bool leaf_inside(cptr<RtLeaf> L, V3 p) {
   int k = L->kind;
   if (k == RT_N_PLANE) return false;                                        // :186-188
   V3 q = xf(L->inv, p);
@@ -74,7 +93,7 @@ __device__ bool leaf_inside(const RtLeaf* L, V3 p) {
          q.y >= L->lo[1] && q.z <= L->hi[2] && q.z >= L->lo[2];
 }
 
-__device__ bool leaf_on_surface(const RtLeaf* L, V3 p) {
+__device__ bool leaf_on_surface(cptr<RtLeaf> L, V3 p) {
   V3 q = xf(L->inv, p);
   int k = L->kind;
   if (k == RT_N_SPHERE) return fabs(len(sub(q, ld3(L->c))) - L->radius) < EPS;   // :76-80
@@ -88,7 +107,7 @@ __device__ bool leaf_on_surface(const RtLeaf* L, V3 p) {
   return false;
 }
 
-__device__ V3 leaf_normal(const RtLeaf* L, V3 p) {
+__device__ V3 leaf_normal(cptr<RtLeaf> L, V3 p) {
   int k = L->kind;
   if (k == RT_N_PLANE) return ld3(L->pn[0]);                               // :182-184
   V3 q = xf(L->inv, p);
@@ -102,7 +121,7 @@ __device__ V3 leaf_normal(const RtLeaf* L, V3 p) {
 }
 
 // MathSphere::get_uv_coordinates (:82-114): the centre is subtracted BEFORE the inverse transform
-__device__ void sphere_uv(const RtLeaf* L, V3 p, double* u, double* v) {
+__device__ void sphere_uv(cptr<RtLeaf> L, V3 p, double* u, double* v) {
   V3 q = xf(L->inv, sub(p, ld3(L->c)));
   q = scale(normalized(q), 1.0 - EPS);
   double phi = acos(-((0.0 * q.x + 1.0 * q.y) + 0.0 * q.z));             // up = (0,1,0)
@@ -115,7 +134,7 @@ __device__ void sphere_uv(const RtLeaf* L, V3 p, double* u, double* v) {
 
 // Candidate hit distances of one primitive for the world ray (ro, rd):
 // RTObject::intersects (rt_object.rs:28-31) = reverse_transform_ray + MathShape::intersects.
-__device__ __forceinline__ int leaf_candidates(const RtLeaf* L, V3 ro, V3 rd, double* t0, double* t1) {
+__device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, double* t0, double* t1) {
   V3 o = xf(L->inv, ro);                                                   // transformation.rs:88-93
   V3 d = sub(xf(L->inv, rd), ld3(L->inv_o));
   int k = L->kind;
@@ -162,23 +181,23 @@ __device__ __forceinline__ int leaf_candidates(const RtLeaf* L, V3 ro, V3 rd, do
 
 // Conjunction of every CSG ancestor's sibling test for a hit of leaf L at world point p
 // (csg.rs:43-95), as a postfix program over a bit stack.
-__device__ bool leaf_filter(const RtDevScene& S, const RtLeaf* L, V3 p) {
+__device__ bool leaf_filter(const DS& S, cptr<RtLeaf> L, V3 p) {
   uint32_t st = 0;
   const int e = L->prog_end;
   for (int k = L->prog_begin; k < e; ++k) {
-    const RtProg pr = S.prog[k];
-    if (pr.op == RT_OP_INSIDE) {
-      st = (st << 1) | (leaf_inside(&S.leaves[pr.arg], p) ? 1u : 0u);
-    } else if (pr.op == RT_OP_REQUIRE) {
+    const int op = S.prog[k].op, arg = S.prog[k].arg;
+    if (op == RT_OP_INSIDE) {
+      st = (st << 1) | (leaf_inside(&S.leaves[arg], p) ? 1u : 0u);
+    } else if (op == RT_OP_REQUIRE) {
       uint32_t v = st & 1u;
       st >>= 1;
-      if (v != (uint32_t)pr.arg) return false;
+      if (v != (uint32_t)arg) return false;
     } else {
       uint32_t b = st & 1u;
       st >>= 1;
       uint32_t a = st & 1u, r;
-      if (pr.op == RT_OP_AND) r = a & b;
-      else if (pr.op == RT_OP_OR) r = a | b;
+      if (op == RT_OP_AND) r = a & b;
+      else if (op == RT_OP_OR) r = a | b;
       else r = a & (b ^ 1u);
       st = (st & ~1u) | r;
     }
@@ -191,7 +210,7 @@ __device__ bool leaf_filter(const RtDevScene& S, const RtLeaf* L, V3 p) {
 // the segment is inside [lo, hi]; boxes are inflated on the host (scene.cpp leaf_box) and tmax
 // carries a relative margin, so f64 rounding here cannot cull a hit the exact code would accept.
 // NaN anywhere makes the comparisons false and the answer "yes" (evaluate exactly).
-__device__ __forceinline__ bool box_may_hit(const double* lo, const double* hi, V3 o, V3 d, V3 inv, double tmax) {
+template <class P> __device__ __forceinline__ bool box_may_hit(P lo, P hi, V3 o, V3 d, V3 inv, double tmax) {
   double tn = 0.0, tf = tmax;
 #define RT_BOXAX(P, D, I, IV)                                                   \
   if (D == 0.0) {                                                               \
@@ -214,17 +233,17 @@ __device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) 
 // Nearest hit over all objects in draw order: accept d if d > EPS && d < nearest
 // (raytracer.rs:141-150).  The acceptance test is pure, so it runs BEFORE the (pure) CSG
 // filter: candidates that cannot win never pay for the sibling is_inside tests.
-__device__ int nearest_hit(const RtDevScene& S, V3 ro, V3 rd, double* dist) {
+__device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist) {
   double best = INFINITY;
   int bobj = -1;
   const V3 inv = {1.0 / rd.x, 1.0 / rd.y, 1.0 / rd.z};
   for (int o = 0; o < S.n_objects; ++o) {
-    const RtObject* O = &S.objects[o];
+    cptr<RtObject> O = &S.objects[o];
     if (O->cull == RT_CULL_ALWAYS) continue;
     if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, ro, rd, inv, cull_tmax(best))) continue;
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
     for (int l = lb; l < le; ++l) {
-      const RtLeaf* L = &S.leaves[l];
+      cptr<RtLeaf> L = &S.leaves[l];
       if (O->leaf_cull) {
         if (L->cull == RT_CULL_ALWAYS) continue;
         if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, ro, rd, inv, cull_tmax(best))) continue;
@@ -247,18 +266,18 @@ __device__ int nearest_hit(const RtDevScene& S, V3 ro, V3 rd, double* dist) {
 // Product of the transparencies of every filtered hit with EPS < d < dist (raytracer.rs:181-197).
 // Early-out once the product is exactly 0 (it stays 0: every factor is finite, checked on the
 // host), objects of transparency exactly 1.0 are skipped (x * 1.0 == x).
-__device__ double shadow_transparency(const RtDevScene& S, V3 p, V3 dir, double dist) {
+__device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
   double tr = 1.0;
   const V3 inv = {1.0 / dir.x, 1.0 / dir.y, 1.0 / dir.z};
   const double tmax = cull_tmax(dist);
   for (int o = 0; o < S.n_objects; ++o) {
-    const RtObject* O = &S.objects[o];
+    cptr<RtObject> O = &S.objects[o];
     if (O->shadow_skip || O->cull == RT_CULL_ALWAYS) continue;
     if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, p, dir, inv, tmax)) continue;
     const double tobj = O->transparency;
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
     for (int l = lb; l < le; ++l) {
-      const RtLeaf* L = &S.leaves[l];
+      cptr<RtLeaf> L = &S.leaves[l];
       if (O->leaf_cull) {
         if (L->cull == RT_CULL_ALWAYS) continue;
         if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, p, dir, inv, tmax)) continue;
@@ -282,67 +301,70 @@ __device__ double shadow_transparency(const RtDevScene& S, V3 p, V3 dir, double 
 // Normal and UV of top-level object O at point p: RTObject shape get_normal / get_uv_coordinates,
 // with CSG's is_on_surface / is_inside evaluated bottom-up over the post-order node list
 // (csg.rs:98-168) and the descent a-then-b of csg.rs:104-121 / :161-167.
-__device__ void object_normal_uv(const RtDevScene& S, const RtObject* O, V3 p, bool want_uv, V3* n,
+__device__ void object_normal_uv(const DS& S, cptr<RtObject> O, V3 p, bool want_uv, V3* n,
                                  double* u, double* v) {
-  const RtNode* N = S.nodes + O->node_begin;
+  cptr<RtNode> N = S.nodes + O->node_begin;
   const int cnt = O->node_count;
   *u = 0.0;
   *v = 0.0;
   if (cnt == 1) {
-    const RtLeaf* L = &S.leaves[N[0].leaf];
+    cptr<RtLeaf> L = &S.leaves[N[0].leaf];
     *n = leaf_normal(L, p);
     if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
     return;
   }
   uint32_t in = 0, on = 0;
   for (int i = 0; i < cnt; ++i) {
-    const RtNode nd = N[i];
+    const int nk = N[i].kind, na = N[i].a, nb = N[i].b, nl = N[i].leaf;
     bool bi, bo;
-    if (nd.kind < RT_N_UNION) {
-      const RtLeaf* L = &S.leaves[nd.leaf];
+    if (nk < RT_N_UNION) {
+      cptr<RtLeaf> L = &S.leaves[nl];
       bi = leaf_inside(L, p);
       bo = leaf_on_surface(L, p);
     } else {
-      bool ia = (in >> nd.a) & 1u, ib = (in >> nd.b) & 1u, oa = (on >> nd.a) & 1u, ob = (on >> nd.b) & 1u;
-      if (nd.kind == RT_N_UNION) { bi = ia || ib; bo = (oa && !ib) || (ob && !ia); }
-      else if (nd.kind == RT_N_INTERSECTION) { bi = ia && ib; bo = (oa && ib) || (ob && ia); }
+      bool ia = (in >> na) & 1u, ib = (in >> nb) & 1u, oa = (on >> na) & 1u, ob = (on >> nb) & 1u;
+      if (nk == RT_N_UNION) { bi = ia || ib; bo = (oa && !ib) || (ob && !ia); }
+      else if (nk == RT_N_INTERSECTION) { bi = ia && ib; bo = (oa && ib) || (ob && ia); }
       else { bi = ia && !ib; bo = (oa && !ib) || (ob && ia); }
     }
     in |= (uint32_t)bi << i;
     on |= (uint32_t)bo << i;
   }
-  int cur = cnt - 1;
+  // Descent a-then-b (csg.rs:104-121, :161-167).  Children precede parents in post-order, so one
+  // downward pass over the node indices visits every lane's path in order; node reads stay
+  // wave-uniform (scalar).  Membership tests go through ballot masks (see trace()).
+  const int lane = __lane_id();
+  int cur = cnt - 1, sel = -1;
   bool neg = false;
-  for (;;) {
-    const RtNode nd = N[cur];
-    if (nd.kind < RT_N_UNION) {
-      const RtLeaf* L = &S.leaves[nd.leaf];
-      *n = leaf_normal(L, p);
-      if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
-      break;
-    }
-    if ((on >> nd.a) & 1u) {
-      cur = nd.a;
-    } else if ((on >> nd.b) & 1u) {
-      if (nd.kind == RT_N_DIFFERENCE) neg = !neg;           // b.get_normal(p) * -1.0
-      cur = nd.b;
-    } else {
-      *n = {1.0, 0.0, 0.0};                                 // fallback; UV is Err -> (0,0)
-      break;
-    }
+  for (int i = cnt - 1; i >= 0; --i) {
+    const int nk = N[i].kind, na = N[i].a, nb = N[i].b, nl = N[i].leaf;
+    if (!((__ballot(cur == i) >> lane) & 1)) continue;
+    if (nk < RT_N_UNION) { sel = nl; cur = -1; }
+    else if ((on >> na) & 1u) cur = na;
+    else if ((on >> nb) & 1u) { if (nk == RT_N_DIFFERENCE) neg = !neg; cur = nb; }   // b.get_normal(p) * -1.0
+    else cur = -1;                                          // fallback (1,0,0); UV is Err -> (0,0)
+  }
+  *n = {1.0, 0.0, 0.0};
+  const int lb = O->leaf_begin, le = lb + O->leaf_count;
+  for (int l = lb; l < le; ++l) {
+    if (!((__ballot(sel == l) >> lane) & 1)) continue;
+    cptr<RtLeaf> L = &S.leaves[l];
+    *n = leaf_normal(L, p);
+    if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
   }
   if (neg) *n = scale(*n, -1.0);
 }
 
 // PixmapTexture::get_color_at (texture.rs:27-34) on RGBA8 texels, /255.0 (sceneparser/texture.rs:29-33)
-__device__ Col texture_color(const RtDevScene& S, int tex, double u, double v) {
-  const RtTexture T = S.textures[tex];
-  double x = u * (double)(T.w - 1);
-  double y = (double)T.h - (v * (double)(T.h - 1)) - 1.0;
+__device__ Col texture_color(const DS& S, int tex, double u, double v) {
+  const int tw = S.textures[tex].w, th = S.textures[tex].h;
+  const int64_t toff = S.textures[tex].offset;
+  double x = u * (double)(tw - 1);
+  double y = (double)th - (v * (double)(th - 1)) - 1.0;
   // `as usize` saturates (NaN/negative -> 0); the reference would panic past the edge: clamp.
-  int xi = x > 0.0 ? (x < (double)(T.w - 1) ? (int)x : T.w - 1) : 0;
-  int yi = y > 0.0 ? (y < (double)(T.h - 1) ? (int)y : T.h - 1) : 0;
-  const uint32_t px = *(const uint32_t*)(S.texels + T.offset + ((size_t)yi * T.w + xi) * 4);
+  int xi = x > 0.0 ? (x < (double)(tw - 1) ? (int)x : tw - 1) : 0;
+  int yi = y > 0.0 ? (y < (double)(th - 1) ? (int)y : th - 1) : 0;
+  const uint32_t px = *(const uint32_t*)(S.texels + toff + ((size_t)yi * tw + xi) * 4);
   return {(double)(px & 0xffu) / 255.0, (double)((px >> 8) & 0xffu) / 255.0, (double)((px >> 16) & 0xffu) / 255.0};
 }
 
@@ -358,10 +380,34 @@ __device__ __forceinline__ V3 refract_dir(V3 i, V3 n, double r, bool* tir) {   /
   return normalized(add(scale(i, r), scale(n, r * cos_1 - cos_2)));
 }
 
+// Normal (normalised, :163), material colour at the UV (:165-170), transparency, reflectivity of
+// each lane's hit object -- SCALARISED over the distinct objects hit in this wave (readlane of the
+// first remaining lane), so every object / node / leaf read is wave-uniform (SMEM, no VGPRs).
+__device__ __forceinline__ void shade_inputs(const DS& S, int oi, V3 p, V3* nrm, Col* c, double* transp,
+                                             double* refl) {
+  uint64_t todo = __ballot(oi >= 0);
+  while (todo) {
+    const int o = __builtin_amdgcn_readlane(oi, (int)__builtin_ctzll(todo));
+    const uint64_t mine = __ballot(oi == o);
+    todo &= ~mine;
+    // test membership through the ballot mask, not `oi == o`: an equality lets the optimiser
+    // substitute the per-lane oi for the uniform o and the loads below turn into VMEM again.
+    if ((mine >> __lane_id()) & 1) {
+      cptr<RtObject> O = &S.objects[o];
+      double u, v;
+      object_normal_uv(S, O, p, O->textured != 0, nrm, &u, &v);
+      *c = O->textured ? texture_color(S, O->tex, u, v) : Col{O->color[0], O->color[1], O->color[2]};
+      *transp = O->transparency;
+      *refl = O->reflectivity;
+    }
+  }
+  *nrm = normalized(*nrm);
+}
+
 // get_ray_color (raytracer.rs:132-287) for one primary ray, recursion unrolled onto a per-lane
 // frame stack.  REFR = the scene has a transparent object (refraction frames need more state).
 template <bool REFR>
-__device__ Col trace(const RtDevScene& S, V3 ro, V3 rd, int max_depth) {
+__device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth) {
   double fA[RT_MAX_DEPTH_CAP][3];     // parent colour already intensified by (1 - w)
   double fW[RT_MAX_DEPTH_CAP];        // child weight w (transparency or reflectivity)
   double fP[REFR ? RT_MAX_DEPTH_CAP : 1][3], fD[REFR ? RT_MAX_DEPTH_CAP : 1][3];
@@ -373,36 +419,68 @@ __device__ Col trace(const RtDevScene& S, V3 ro, V3 rd, int max_depth) {
     bool descend = false;
     double t_hit;
     const int oi = nearest_hit(S, ro, rd, &t_hit);
+#ifdef RT_ABLATE_TRAVERSAL_ONLY          // diagnostic builds only (tools/ablation): cost split
+    return Col{t_hit * 1e-3, (double)oi, 0.0};
+#endif
+    const V3 p = add(ro, scale(rd, t_hit));                               // :162
+    V3 nrm = {0.0, 0.0, 0.0};
+    Col c = {0.0, 0.0, 0.0}, L = {0.0, 0.0, 0.0};
+    double transp = 0.0, refl = 0.0;
+    if (oi >= 0) {
+      // Evaluation order is free (every step is a pure function of the hit), so the shadow
+      // rays of a group of lights are traced FIRST, while only the hit point is live, and the
+      // normal / UV / material and the per-light Lambert terms are formed afterwards: far fewer
+      // registers live across the traversals.  Light accumulation order is unchanged.
+      bool have_shading = false;
+      for (int base = 0; base < S.n_lights; base += RT_LIGHT_GROUP) {
+        double tr[RT_LIGHT_GROUP];
+#pragma unroll
+        for (int k = 0; k < RT_LIGHT_GROUP; ++k) tr[k] = 0.0;
+        const int nk = S.n_lights - base < RT_LIGHT_GROUP ? S.n_lights - base : RT_LIGHT_GROUP;
+#pragma unroll 1
+        for (int k = 0; k < nk; ++k) {                                   // ONE traversal body in the code
+          const V3 lv = sub(ld3(S.lights[base + k].p), p);
+#ifdef RT_ABLATE_NO_SHADOWS
+          const double t = lv.x > 1e300 ? 0.5 : 1.0;
+#else
+          const double t = shadow_transparency(S, p, normalized(lv), len(lv));   // :176-197
+#endif
+#pragma unroll
+          for (int j = 0; j < RT_LIGHT_GROUP; ++j) tr[j] = j == k ? t : tr[j];   // registers, no scratch
+        }
+        if (!have_shading) {
+          shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
+          L = cmul(c, in_range(0.6, 0.6, 0.6));                           // ambient (:172)
+          have_shading = true;
+        }
+#pragma unroll
+        for (int k = 0; k < RT_LIGHT_GROUP; ++k) {                       // :199-227
+          if (base + k >= S.n_lights || tr[k] == 0.0) continue;
+          cptr<RtLight> lt = &S.lights[base + k];
+          const V3 sdir = normalized(sub(ld3(lt->p), p));
+          double ang = acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
+          if (ang >= PI_D / 2.0) ang = PI_D - ang;
+          const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
+          const Col lc = intensify(intensify(Col{lt->col[0], lt->col[1], lt->col[2]}, inten), tr[k]);
+          L = cadd(L, cmul(c, lc));
+        }
+      }
+      if (!have_shading) {
+        shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
+        L = cmul(c, in_range(0.6, 0.6, 0.6));
+      }
+    }
     if (oi < 0) {
       C = {0.0, 0.0, 0.0};                                               // Color::BLACK (:152-160)
     } else {
-      const RtObject* O = &S.objects[oi];
-      const V3 p = add(ro, scale(rd, t_hit));                             // :162
-      V3 nrm;
-      double u, v;
-      object_normal_uv(S, O, p, O->textured != 0, &nrm, &u, &v);
-      nrm = normalized(nrm);                                              // :163
-      Col c = O->textured ? texture_color(S, O->tex, u, v) : Col{O->color[0], O->color[1], O->color[2]};
-      Col L = cmul(c, in_range(0.6, 0.6, 0.6));                           // ambient (:172)
-      for (int li = 0; li < S.n_lights; ++li) {                           // :175-228
-        const RtLight lt = S.lights[li];
-        const V3 lp = ld3(lt.p);
-        const V3 lv = sub(lp, p);
-        const V3 sdir = normalized(lv);
-        const double dist = len(lv);
-        const double tr = shadow_transparency(S, p, sdir, dist);
-        if (tr == 0.0) continue;
-        double ang = acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
-        if (ang >= PI_D / 2.0) ang = PI_D - ang;
-        const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
-        const Col lc = intensify(intensify(Col{lt.col[0], lt.col[1], lt.col[2]}, inten), tr);
-        L = cadd(L, cmul(c, lc));
-      }
       const V3 nd = scale(rd, -1.0);                                      // :230-235
-      const bool inside = acos(dot(nd, nrm) / (len(nd) * len(nrm))) >= PI_D / 2.0;
+      // angle(-dir, n) >= PI/2 (:230-231).  acos is monotone and ocml's is within 2 ulp, so for
+      // |cos| > 1e-15 (>= 4 ulp of PI/2 away from the threshold) the sign of the cosine decides
+      // exactly; only near-grazing hits (and NaN) evaluate the acos itself.
+      const double cin = dot(nd, nrm) / (len(nd) * len(nrm));
+      const bool inside = cin < -1e-15 ? true : (cin > 1e-15 ? false : acos(cin) >= PI_D / 2.0);
       const V3 n2 = inside ? scale(nrm, -1.0) : nrm;
       const double r1 = inside ? 1.45 : 1.0, r2 = inside ? 1.0 : 1.45;
-      const double transp = O->transparency, refl = O->reflectivity;
       bool tir = false;
       V3 tdir = {0.0, 0.0, 0.0};
       const bool do_refr = REFR && depth < max_depth && transp != 0.0;   // :242
@@ -465,6 +543,21 @@ __device__ Col trace(const RtDevScene& S, V3 ro, V3 rd, int max_depth) {
   }
 }
 
+__device__ __forceinline__ DS make_ds(const RtDevScene& s) {
+  DS d;
+  d.objects = as_const(s.objects);
+  d.nodes = as_const(s.nodes);
+  d.leaves = as_const(s.leaves);
+  d.prog = as_const(s.prog);
+  d.lights = as_const(s.lights);
+  d.textures = as_const(s.textures);
+  d.texels = s.texels;
+  d.n_objects = s.n_objects;
+  d.n_lights = s.n_lights;
+  d.shadow_early_out = s.shadow_early_out;
+  return d;
+}
+
 // PerspectiveCamera::create_ray (camera.rs:65-74)
 __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double y, V3* ro, V3* rd) {
   double sx = ((x / cam.width) - 0.5) * cam.aspect;
@@ -494,7 +587,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
   if (y >= S.height) return;
   V3 ro, rd;
   camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
-  const Col c = trace<REFR>(S, ro, rd, max_depth);
+  const Col c = trace<REFR>(make_ds(S), ro, rd, max_depth);
   uint8_t* row = out + (size_t)r * stride;
   if constexpr (F64) {
     double* o = (double*)row + (size_t)x * 4;
@@ -511,7 +604,7 @@ __global__ __launch_bounds__(256) void render_points_kernel(RtDevScene S, const 
   if (i >= n) return;
   V3 ro, rd;
   camera_ray(S.cam, xy[2 * i], xy[2 * i + 1], &ro, &rd);
-  const Col c = trace<REFR>(S, ro, rd, max_depth);
+  const Col c = trace<REFR>(make_ds(S), ro, rd, max_depth);
   out[4 * i] = c.r; out[4 * i + 1] = c.g; out[4 * i + 2] = c.b; out[4 * i + 3] = 1.0;
 }
 

@@ -4,7 +4,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import tinyraytracerinrust_amd as T
 S = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "scenes")
-for (W, H, d, scene) in [(3840, 2160, 10, "globes"), (1920, 1080, 5, "globes"), (1920, 1080, 0, None)]:
+CASES = [(3840, 2160, 10, "globes"), (3840, 2160, 0, "globes"), (1920, 1080, 5, "globes"), (1920, 1080, 0, None)]
+for (W, H, d, scene) in CASES:
     rt = T.RayTracer(W, H)
     if scene:
         rt.load_scene(open(os.path.join(S, scene + ".scene")).read(), 0.0, asset_dir=S)
