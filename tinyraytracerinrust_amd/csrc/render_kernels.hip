@@ -6,7 +6,8 @@
 // tile.  All arithmetic is IEEE f64 with NO contraction (Rust never fuses): the file is
 // compiled with -ffp-contract=off and the pragma below.  sqrt and division lower to correctly
 // rounded sequences on gfx950 (verified bit-exact against glibc, profiles/r01_libm_probe.txt);
-// acos/sin come from ocml and may differ from glibc by 1 ulp (DESIGN.md "Parity").
+// acos is rt_acos (rt_math.h: 1 ulp from glibc on ~0.4% of inputs, and far fewer registers than
+// ocml's); sin comes from ocml and may differ from glibc by 1 ulp (DESIGN.md "Parity").
 //
 // The reference's recursion (get_ray_color calling itself for refraction and reflection,
 // raytracer.rs:242-280) becomes an explicit per-lane frame stack combined in the same
@@ -20,7 +21,9 @@
 
 #include <vector>
 
+#define RT_HD __device__
 #include "rt_blob.h"
+#include "rt_math.h"
 #include "scene.h"
 
 #pragma clang fp contract(off)
@@ -124,9 +127,9 @@ __device__ V3 leaf_normal(cptr<RtLeaf> L, V3 p) {
 __device__ void sphere_uv(cptr<RtLeaf> L, V3 p, double* u, double* v) {
   V3 q = xf(L->inv, sub(p, ld3(L->c)));
   q = scale(normalized(q), 1.0 - EPS);
-  double phi = acos(-((0.0 * q.x + 1.0 * q.y) + 0.0 * q.z));             // up = (0,1,0)
+  double phi = rt_acos(-((0.0 * q.x + 1.0 * q.y) + 0.0 * q.z));             // up = (0,1,0)
   if (isnan(phi)) phi = 0.0;
-  double theta = (acos(((q.x * 0.0 + q.y * 0.0) + q.z * -1.0) / sin(phi))) / (2.0 * PI_D);   // u_zero = (0,0,-1)
+  double theta = (rt_acos(((q.x * 0.0 + q.y * 0.0) + q.z * -1.0) / sin(phi))) / (2.0 * PI_D);   // u_zero = (0,0,-1)
   if (isnan(theta)) theta = 0.0;
   *v = phi / PI_D;
   *u = ((-1.0 * q.x + 0.0 * q.y) + 0.0 * q.z > 0.0) ? 1.0 - theta : theta;  // u_qrtr = (-1,0,0)
@@ -458,7 +461,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth) {
           if (base + k >= S.n_lights || tr[k] == 0.0) continue;
           cptr<RtLight> lt = &S.lights[base + k];
           const V3 sdir = normalized(sub(ld3(lt->p), p));
-          double ang = acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
+          double ang = rt_acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
           if (ang >= PI_D / 2.0) ang = PI_D - ang;
           const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
           const Col lc = intensify(intensify(Col{lt->col[0], lt->col[1], lt->col[2]}, inten), tr[k]);
@@ -474,11 +477,11 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth) {
       C = {0.0, 0.0, 0.0};                                               // Color::BLACK (:152-160)
     } else {
       const V3 nd = scale(rd, -1.0);                                      // :230-235
-      // angle(-dir, n) >= PI/2 (:230-231).  acos is monotone and ocml's is within 2 ulp, so for
+      // angle(-dir, n) >= PI/2 (:230-231).  acos is monotone and rt_acos is within 1 ulp, so for
       // |cos| > 1e-15 (>= 4 ulp of PI/2 away from the threshold) the sign of the cosine decides
       // exactly; only near-grazing hits (and NaN) evaluate the acos itself.
       const double cin = dot(nd, nrm) / (len(nd) * len(nrm));
-      const bool inside = cin < -1e-15 ? true : (cin > 1e-15 ? false : acos(cin) >= PI_D / 2.0);
+      const bool inside = cin < -1e-15 ? true : (cin > 1e-15 ? false : rt_acos(cin) >= PI_D / 2.0);
       const V3 n2 = inside ? scale(nrm, -1.0) : nrm;
       const double r1 = inside ? 1.45 : 1.0, r2 = inside ? 1.0 : 1.45;
       bool tir = false;
