@@ -28,6 +28,22 @@
 
 #pragma clang fp contract(off)
 
+// Diagnostic section-cycle build (make profile-sections; never the product): wave-cycles spent
+// in each part of trace(), summed over all waves with one atomic per wave per section entry.
+#ifdef RT_PROF
+__device__ unsigned long long g_rt_prof[8];
+#define PROF_T0(v) const long long v = clock64()
+#define PROF_ADD(sec, v)                                                              \
+  do {                                                                                \
+    const long long d_ = clock64() - (v);                                             \
+    if ((int)__lane_id() == __ffsll((long long)__ballot(1)) - 1)                       \
+      atomicAdd(&g_rt_prof[sec], (unsigned long long)d_);                             \
+  } while (0)
+#else
+#define PROF_T0(v) (void)0
+#define PROF_ADD(sec, v) (void)0
+#endif
+
 namespace {
 
 // Scene tables are read-only for the whole launch: view them through the CONSTANT address space
@@ -214,6 +230,27 @@ __device__ bool leaf_filter(const DS& S, cptr<RtLeaf> L, V3 p) {
 // carries a relative margin, so f64 rounding here cannot cull a hit the exact code would accept.
 // NaN anywhere makes the comparisons false and the answer "yes" (evaluate exactly).
 template <class P> __device__ __forceinline__ bool box_may_hit(P lo, P hi, V3 o, V3 d, V3 inv, double tmax) {
+#ifndef RT_BRANCHY_BOX
+  // Select form (no exec-mask branches).  An axis with d == 0 only asks whether the origin lies
+  // in the slab; otherwise the usual interval narrowing, where a NaN bound narrows nothing.
+  double tn = 0.0, tf = tmax;
+  bool out = false;
+#define RT_BOXAX(P, D, I, IV)                                                   \
+  {                                                                             \
+    const double a = (lo[I] - P) * IV, b = (hi[I] - P) * IV;                    \
+    const bool z = D == 0.0;                                                    \
+    out = out || (z && (P < lo[I] || P > hi[I]));                               \
+    const bool sw = a > b;                                                      \
+    const double mn = sw ? b : a, mx = sw ? a : b;                              \
+    tn = (!z && mn > tn) ? mn : tn;                                             \
+    tf = (!z && mx < tf) ? mx : tf;                                             \
+  }
+  RT_BOXAX(o.x, d.x, 0, inv.x)
+  RT_BOXAX(o.y, d.y, 1, inv.y)
+  RT_BOXAX(o.z, d.z, 2, inv.z)
+#undef RT_BOXAX
+  return !out && !(tn > tf);
+#else
   double tn = 0.0, tf = tmax;
 #define RT_BOXAX(P, D, I, IV)                                                   \
   if (D == 0.0) {                                                               \
@@ -229,7 +266,20 @@ template <class P> __device__ __forceinline__ bool box_may_hit(P lo, P hi, V3 o,
   RT_BOXAX(o.z, d.z, 2, inv.z)
 #undef RT_BOXAX
   return !(tn > tf);
+#endif
 }
+// Reciprocal for the culling slabs only (never for a value the reference computes): hardware
+// rcp + one Newton step, ~1e-15 relative -- far inside the culling margins.  d == 0 -> NaN or
+// inf, which box_may_hit never reads (that axis takes the d == 0 branch).
+__device__ __forceinline__ double cull_rcp(double x) {
+#ifdef RT_EXACT_CULL_RCP
+  return 1.0 / x;
+#else
+  const double r = __builtin_amdgcn_rcp(x);
+  return fma(r, fma(-x, r, 1.0), r);
+#endif
+}
+__device__ __forceinline__ V3 cull_inv(V3 d) { return {cull_rcp(d.x), cull_rcp(d.y), cull_rcp(d.z)}; }
 __device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) + 1e-7; }
 
 // ------------------------------------------------------------------ traversal (raytracer.rs)
@@ -239,7 +289,7 @@ __device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) 
 __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist) {
   double best = INFINITY;
   int bobj = -1;
-  const V3 inv = {1.0 / rd.x, 1.0 / rd.y, 1.0 / rd.z};
+  const V3 inv = cull_inv(rd);
   for (int o = 0; o < S.n_objects; ++o) {
     cptr<RtObject> O = &S.objects[o];
     if (O->cull == RT_CULL_ALWAYS) continue;
@@ -271,7 +321,7 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist) {
 // host), objects of transparency exactly 1.0 are skipped (x * 1.0 == x).
 __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
   double tr = 1.0;
-  const V3 inv = {1.0 / dir.x, 1.0 / dir.y, 1.0 / dir.z};
+  const V3 inv = cull_inv(dir);
   const double tmax = cull_tmax(dist);
   for (int o = 0; o < S.n_objects; ++o) {
     cptr<RtObject> O = &S.objects[o];
@@ -418,10 +468,15 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth) {
   int fPend[REFR ? RT_MAX_DEPTH_CAP : 1];
   int sp = 0, depth = 0;
   Col C = {0.0, 0.0, 0.0};
+  [[maybe_unused]] int trip = 0;
   for (;;) {
     bool descend = false;
     double t_hit;
+    PROF_T0(p0);
     const int oi = nearest_hit(S, ro, rd, &t_hit);
+    PROF_ADD(trip == 0 ? 0 : 1, p0);
+    ++trip;
+    PROF_T0(p1);
 #ifdef RT_ABLATE_TRAVERSAL_ONLY          // diagnostic builds only (tools/ablation): cost split
     return Col{t_hit * 1e-3, (double)oi, 0.0};
 #endif
@@ -446,13 +501,17 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth) {
 #ifdef RT_ABLATE_NO_SHADOWS
           const double t = lv.x > 1e300 ? 0.5 : 1.0;
 #else
+          PROF_T0(p2);
           const double t = shadow_transparency(S, p, normalized(lv), len(lv));   // :176-197
+          PROF_ADD(2, p2);
 #endif
 #pragma unroll
           for (int j = 0; j < RT_LIGHT_GROUP; ++j) tr[j] = j == k ? t : tr[j];   // registers, no scratch
         }
         if (!have_shading) {
+          PROF_T0(p3);
           shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
+          PROF_ADD(3, p3);
           L = cmul(c, in_range(0.6, 0.6, 0.6));                           // ambient (:172)
           have_shading = true;
         }
@@ -522,6 +581,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth) {
         C = L;
       }
     }
+    PROF_ADD(4, p1);
     if (descend) continue;
     while (sp > 0) {                                                      // post-order combine
       const int f = sp - 1;
@@ -580,6 +640,10 @@ template <bool REFR, bool F64>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU))) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
                                                           int n_rows, int max_depth, uint8_t* __restrict__ out,
                                                           size_t stride) {
+#ifdef RT_DIAG_LDS                       // diagnostic builds only: cap occupancy with an LDS pad
+  __shared__ volatile char rt_pad[RT_DIAG_LDS];
+  if (threadIdx.x == 0) rt_pad[0] = 0;
+#endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tiles_x = (S.width + 15) >> 4;
   const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
@@ -589,8 +653,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
   const int y = y_first + (r / band_rows) * band_pitch + r % band_rows;
   if (y >= S.height) return;
   V3 ro, rd;
+  PROF_T0(p5);
   camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
   const Col c = trace<REFR>(make_ds(S), ro, rd, max_depth);
+  PROF_ADD(5, p5);
   uint8_t* row = out + (size_t)r * stride;
   if constexpr (F64) {
     double* o = (double*)row + (size_t)x * 4;
@@ -664,6 +730,17 @@ static size_t put(std::vector<uint8_t>& blob, const std::vector<T>& v) {
 }
 
 extern "C" {
+
+#ifdef RT_PROF
+// Diagnostic build only: read-and-reset the section wave-cycle counters (tools/section_profile.py).
+__attribute__((visibility("default"))) int rt_diag_prof(unsigned long long* out8) {
+  if (hipDeviceSynchronize() != hipSuccess) return RT_ERR_DEVICE;
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_rt_prof), 8 * sizeof(unsigned long long)) != hipSuccess) return RT_ERR_DEVICE;
+  static const unsigned long long zero[8] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_rt_prof), zero, sizeof(zero)) != hipSuccess) return RT_ERR_DEVICE;
+  return RT_OK;
+}
+#endif
 
 int rt_device_count(int* count) {
   if (!count) return fail(RT_ERR_INVALID, "null output");
