@@ -59,6 +59,20 @@ typedef struct rt_material {         /* SolidColorMaterial / TexturedMaterial (m
   double transparency;
 } rt_material;
 
+typedef struct rt_ray_record {       /* one RayDebuggerCallback call (raytracer.rs:17-19) as RayInfo */
+  int32_t depth;
+  int32_t ray_type;                  /* RayType: 0 NormalRay, 1 ReflectionRay, 2 TransmissionRay */
+  int32_t object;                    /* intersected object, draw index; -1 = none */
+  int32_t intersected;               /* distance != INFINITY (ray_debugger.rs:105) */
+  int32_t has_normal;
+  int32_t pad;
+  double point[3], direction[3];     /* the ray */
+  double distance;                   /* INFINITY on a miss */
+  double intersection[3];            /* point + direction * (distance, or 1000 on a miss) */
+  double normal[3];                  /* object shape's get_normal at the intersection (not normalised) */
+  double color[4];                   /* the colour get_ray_color returns for this ray */
+} rt_ray_record;
+
 typedef struct rt_scene rt_scene;    /* a RayTracer (raytracer.rs:21-35): objects, lights, camera */
 typedef struct rt_ctx rt_ctx;        /* per-device context: device scene, scratch, timing events */
 
@@ -147,6 +161,36 @@ int rt_render_rows_f64(rt_ctx* ctx, uint32_t y0, uint32_t y1, int32_t max_depth,
  * antialiaser.rs:108-112): xy = n pairs of doubles, out = n x 4 doubles. Device or host. */
 int rt_render_points_f64(rt_ctx* ctx, const double* xy, size_t n, int32_t max_depth,
                          double* rgba_f64, void* stream);
+/* Ray-debugger recording (RayDebugger::record_rays, ray_debugger.rs:92-137): trace pixel (x, y)
+ * (fractional allowed) once with the debugger callback attached and return one record per ray in
+ * the reference's callback order (a ray reports after its children).  *n_rays = rays traced
+ * (records past cap are dropped); rgba (may be NULL) = get_pixel's colour.  Host pointers;
+ * synchronous.  Not a throughput path. */
+int rt_record_rays(rt_ctx* ctx, double x, double y, int32_t max_depth, rt_ray_record* records, int32_t cap,
+                   int32_t* n_rays, double* rgba);
+/* Orthogonal preview view (DebugWindow::render_orthogonal_view_line, debug_window.rs:166-227)
+ * for rows [y0, y1) at the scene's W x H: per pixel a ray from 10000 along the third axis with
+ * origin[axis1] = ((x - W/2) * dir1) / scale, origin[axis2] = ((y - H/2) * dir2) / scale; the
+ * object with the smallest intersection distance (any sign, no EPS) gives its flat colour
+ * (RTObject::get_color, rt_object.rs:45-47), a miss is (0,0,0,0).  The GUI's views are
+ * OrthoAxes (ray_debugger.rs:33-68): top (0,2,+1,-1,2), front (0,1,+1,-1,2), side (2,1,-1,-1,2).
+ * Either output may be NULL (not both); device or host pointers.  RT_ERR_INVALID for invalid
+ * axes (the reference panics). */
+int rt_render_ortho(rt_ctx* ctx, int32_t axis1, int32_t axis2, double dir1, double dir2, double scale,
+                    uint32_t y0, uint32_t y1, uint8_t* rgba8, size_t row_stride_bytes, double* rgba_f64,
+                    size_t f64_stride, void* stream);
+/* Adaptive anti-aliasing pass (antialiaser.rs:87-191, driven as debug_window.rs:275-320) over a
+ * QUANTISED frame of the uploaded scene's size: corners come from src (u8 / 255), interior
+ * sub-pixels are traced at (x + i/size, y + j/size), size = 2^level + 1; a cell subdivides while
+ * the mean |dRGBA| of its corners exceeds threshold and level > 0.  Writes the whole frame to
+ * dst_rgba8 and/or dst_f64 (either may be NULL, not both); the last column and row are the source
+ * pixels (the reference never anti-aliases them).  level <= 4.  *rays_traced (may be NULL) = the
+ * reference's ray_counter.  Pointers may be device or host; the call returns when the frame is
+ * done (the pass sizes its work from the edge count).  Replaces AntiAliaser::get_anti_aliased_pixel
+ * over every pixel (antialiaser.rs:53-71, :87-122). */
+int rt_antialias(rt_ctx* ctx, const uint8_t* src_rgba8, size_t src_stride, double threshold, int32_t level,
+                 int32_t max_depth, uint8_t* dst_rgba8, size_t dst_stride, double* dst_f64, size_t f64_stride,
+                 uint64_t* rays_traced, void* stream);
 /* Milliseconds of the last render launch on this context (HIP events recorded on the launch's
  * stream around the kernel). */
 int rt_ctx_last_kernel_ms(rt_ctx* ctx, float* ms);

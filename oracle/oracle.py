@@ -71,6 +71,13 @@ def _lib(counting: bool = False):
                                   ctypes.POINTER(ctypes.c_double)]
     lib.orc_render_rows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    lib.orc_render_ortho.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    lib.orc_record_rays.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_void_p, ctypes.c_int,
+                                    ctypes.c_void_p]
+    lib.orc_antialias.restype = ctypes.c_longlong
+    lib.orc_antialias.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_double,
+                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     lib.orc_register_texture.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     _libs[key] = lib
     return lib
@@ -169,3 +176,38 @@ class OracleScene:
         if self.counting:
             return of, ou, dict(zip(COUNTER_NAMES, (int(c) for c in cnt)))
         return of, ou
+
+    def antialias(self, frame_u8: np.ndarray, threshold: float = 0.01, level: int = 3, threads: int = 0,
+                  f64: bool = True):
+        """Adaptive anti-aliasing of a quantised (H, W, 4) RGBA8 frame (antialiaser.rs:87-191).
+        Returns (f64 or None, u8, sub-pixel rays traced)."""
+        fr = np.ascontiguousarray(frame_u8, dtype=np.uint8)
+        assert fr.shape == (self.height, self.width, 4)
+        if threads <= 0:
+            threads = default_threads()
+        of = np.zeros((self.height, self.width, 4), np.float64) if f64 else None
+        ou = np.zeros((self.height, self.width, 4), np.uint8)
+        rays = self.lib.orc_antialias(self.h, fr.ctypes.data, self.width * 4, float(threshold), int(level),
+                                      of.ctypes.data if of is not None else None, ou.ctypes.data, threads)
+        if rays < 0:
+            raise ValueError("unsupported anti-aliasing level")
+        return of, ou, int(rays)
+
+    def render_ortho(self, axis1: int, axis2: int, dir1: float, dir2: float, scale: float = 2.0,
+                     y0: int = 0, y1: int | None = None):
+        """Orthogonal preview rows (debug_window.rs:166-227). Returns (f64, u8)."""
+        y1 = self.height if y1 is None else y1
+        of = np.zeros((y1 - y0, self.width, 4), np.float64)
+        ou = np.zeros((y1 - y0, self.width, 4), np.uint8)
+        if self.lib.orc_render_ortho(self.h, axis1, axis2, dir1, dir2, scale, y0, y1, of.ctypes.data, ou.ctypes.data):
+            raise ValueError("Invalid axes")
+        return of, ou
+
+    def record_rays(self, x: float, y: float, cap: int = 1 << 17):
+        """Ray-debugger records of one pixel (callback order) as raw bytes of the C struct; the
+        caller views them with the product's RAY_RECORD_DTYPE (identical layout)."""
+        size = self.lib.orc_ray_record_size()
+        buf = np.zeros(cap * size, np.uint8)
+        rgba = (ctypes.c_double * 4)()
+        n = self.lib.orc_record_rays(self.h, float(x), float(y), buf.ctypes.data, cap, rgba)
+        return buf[:min(n, cap) * size], np.array(rgba[:])

@@ -1128,3 +1128,51 @@ def load_texture(rgba8) -> tuple:
     h, w = rgba8.shape[:2]
     flat = rgba8.reshape(-1, 4).tolist()
     return (w, h, [Color(p[0] / 255.0, p[1] / 255.0, p[2] / 255.0, p[3] / 255.0) for p in flat])
+
+
+def antialias(scene, frame_u8, threshold=0.01, level=3):
+    """antialiaser.rs:87-191 over a quantised frame (list of rows of (r, g, b, a) u8 tuples),
+    as debug_window.rs:275-320 drives it.  Returns (rows of Color, rays traced); the last row and
+    column are the source colours."""
+    H, W = len(frame_u8), len(frame_u8[0])
+    size = (1 << level) + 1
+
+    def src(x, y):                                                  # easy_pixbuf.rs:55-64
+        p = frame_u8[y][x]
+        return Color(p[0] / 255.0, p[1] / 255.0, p[2] / 255.0, p[3] / 255.0)
+
+    def different(c1, c2):                                          # antialiaser.rs:154-162
+        return (abs(c1.r - c2.r) + abs(c1.g - c2.g) + abs(c1.b - c2.b) + abs(c1.a - c2.a)) / 4.0 > threshold
+
+    def average(c1, c2, c3, c4):                                    # antialiaser.rs:164-171
+        return Color((c1.r + c2.r + c3.r + c4.r) / 4.0, (c1.g + c2.g + c3.g + c4.g) / 4.0,
+                     (c1.b + c2.b + c3.b + c4.b) / 4.0, (c1.a + c2.a + c3.a + c4.a) / 4.0)
+
+    rays = 0
+    out = []
+    for y in range(H - 1):
+        row = []
+        for x in range(W - 1):
+            n = size - 1
+            memo = {(0, 0): src(x, y), (0, n): src(x, y + 1), (n, 0): src(x + 1, y), (n, n): src(x + 1, y + 1)}
+
+            def sub(sx, sy):
+                nonlocal rays
+                if (sx, sy) not in memo:
+                    rays += 1
+                    memo[(sx, sy)] = scene.rt.get_pixel(x + (sx / size), y + (sy / size))
+                return memo[(sx, sy)]
+
+            def cell(x1, y1, x2, y2, lv):
+                c1, c2, c3, c4 = sub(x1, y1), sub(x2, y1), sub(x1, y2), sub(x2, y2)
+                if not (different(c1, c2) or different(c1, c3) or different(c1, c4)) or lv <= 0:
+                    return average(c1, c2, c3, c4)
+                mx, my = x1 + (x2 - x1) // 2, y1 + (y2 - y1) // 2
+                return average(cell(x1, y1, mx, my, lv - 1), cell(mx, y1, x2, my, lv - 1),
+                               cell(x1, my, mx, y2, lv - 1), cell(mx, my, x2, y2, lv - 1))
+
+            row.append(cell(0, 0, n, n, level))
+        row.append(src(W - 1, y))
+        out.append(row)
+    out.append([src(x, H - 1) for x in range(W)])
+    return out, rays

@@ -676,14 +676,46 @@ static Vec refracted_dir(Vec incident, Vec normal, double r, int *tir) {        
   return v_normalized(result);
 }
 
-static Color get_ray_color(const orc_scene *sc, Ray ray, int depth) {               /* raytracer.rs:132-287 */
+/* Ray-debugger callback (raytracer.rs:17-19; consumer ray_debugger.rs:92-137): when set, each
+ * finished ray appends one record, in the reference's callback order. */
+typedef struct {
+  int depth, ray_type, object, intersected, has_normal, pad;
+  double point[3], direction[3], distance, intersection[3], normal[3], color[4];
+} OrcRayRecord;
+typedef struct { const orc_scene *sc; OrcRayRecord *out; int cap, n; } OrcRec;
+static __thread OrcRec *g_rec;
+
+static void debugger_cb(int depth, Ray ray, double distance, const RTObject *obj, Color color, int ray_type) {
+  OrcRec *r = g_rec;
+  int i = r->n++;
+  if (i >= r->cap) return;
+  OrcRayRecord *o = &r->out[i];
+  memset(o, 0, sizeof *o);
+  o->depth = depth; o->ray_type = ray_type; o->distance = distance;
+  o->object = obj ? (int)(obj - r->sc->objects) : -1;
+  o->intersected = distance != INFINITY;                                           /* ray_debugger.rs:105 */
+  Vec ip = v_add(ray.point, v_scale(ray.direction, o->intersected ? distance : 1000.0));
+  o->point[0] = ray.point.x; o->point[1] = ray.point.y; o->point[2] = ray.point.z;
+  o->direction[0] = ray.direction.x; o->direction[1] = ray.direction.y; o->direction[2] = ray.direction.z;
+  o->intersection[0] = ip.x; o->intersection[1] = ip.y; o->intersection[2] = ip.z;
+  if (obj) {
+    Vec n = shape_get_normal(obj->shape, ip);                                       /* :113-119, not normalised */
+    o->has_normal = 1; o->normal[0] = n.x; o->normal[1] = n.y; o->normal[2] = n.z;
+  }
+  o->color[0] = color.r; o->color[1] = color.g; o->color[2] = color.b; o->color[3] = color.a;
+}
+
+static Color get_ray_color(const orc_scene *sc, Ray ray, int depth, int ray_type) { /* raytracer.rs:132-287 */
   NearestCtx nc = {INFINITY, NULL, NULL};
   for (int i = 0; i < sc->n_objects; ++i) {
     nc.cur = &sc->objects[i];
     rtobject_intersects(&sc->objects[i], ray, add_nearest, &nc);
   }
   const RTObject *obj = nc.nearest_obj;
-  if (!obj) return BLACK;                                                           /* :152-160 */
+  if (!obj) {                                                                       /* :152-160 */
+    if (g_rec) debugger_cb(depth, ray, INFINITY, NULL, BLACK, ray_type);
+    return BLACK;
+  }
   double nearest_distance = nc.nearest;
 
   CNT(C_SHADE);
@@ -735,7 +767,7 @@ static Color get_ray_color(const orc_scene *sc, Ray ray, int depth) {           
     refracted.direction = refracted_dir(ray.direction, normal, r1 / r2, &tir);
     if (!tir) {
       CNT(C_RAY_REFRACT); CNT(C_COMBINE);
-      Color rc = get_ray_color(sc, refracted, depth + 1);
+      Color rc = get_ray_color(sc, refracted, depth + 1, 2);   /* TransmissionRay */
       FL(1);
       final_light = c_add(c_intensify(final_light, 1.0 - transparency), c_intensify(rc, transparency));
     }
@@ -747,16 +779,17 @@ static Color get_ray_color(const orc_scene *sc, Ray ray, int depth) {           
     reflected.point = v_add(ray.point, v_scale(ray.direction, nearest_distance));
     reflected.direction = reflected_dir(ray.direction, normal);
     CNT(C_RAY_REFLECT); CNT(C_COMBINE);
-    Color rc = get_ray_color(sc, reflected, depth + 1);
+    Color rc = get_ray_color(sc, reflected, depth + 1, 1);   /* ReflectionRay */
     FL(1);
     final_light = c_add(c_intensify(final_light, 1.0 - reflectivity), c_intensify(rc, reflectivity));
   }
+  if (g_rec) debugger_cb(depth, ray, nearest_distance, obj, final_light, ray_type);   /* :282-284 */
   return final_light;
 }
 
 static Color get_pixel(const orc_scene *sc, double x, double y) {                  /* raytracer.rs:359-363, camera.rs:58-63 */
   CNT(C_RAY_PRIMARY);
-  return get_ray_color(sc, camera_create_ray(&sc->camera, x, y), 0);
+  return get_ray_color(sc, camera_create_ray(&sc->camera, x, y), 0, 0);
 }
 
 /* ========================================================================= */
@@ -1683,3 +1716,190 @@ int orc_render_rows(const orc_scene *sc, int y0, int y1, int row_step, double *f
 
 int orc_num_counters(void) { return C_NUM; }
 int orc_counting_build(void) { return ORC_COUNTERS; }
+
+/* ------------------------------------------------------------------------- */
+/* Adaptive anti-aliasing (antialiaser.rs), restated depth-first with the     */
+/* reference's per-pixel memo grid.  Input = the QUANTISED frame re-read as   */
+/* u8/255 colours (debug_window.rs:280-286, easy_pixbuf.rs:55-64).            */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  const orc_scene *sc;
+  const uint8_t *src; size_t stride;
+  double threshold; int level, size;
+  int x, y;
+  Color *grid; unsigned char *have;     /* sub_pixels[sub_x][sub_y]: Option<Color> */
+  uint64_t rays;
+} AaPixel;
+
+static Color aa_src(const AaPixel *a, int x, int y) {                 /* easy_pixbuf.rs:55-64 */
+  const uint8_t *p = a->src + (size_t)y * a->stride + (size_t)x * 4;
+  Color c = {p[0] / 255.0, p[1] / 255.0, p[2] / 255.0, p[3] / 255.0};
+  return c;
+}
+
+static int aa_different(Color c1, Color c2, double threshold) {         /* antialiaser.rs:154-162 */
+  return (fabs(c1.r - c2.r) + fabs(c1.g - c2.g) + fabs(c1.b - c2.b) + fabs(c1.a - c2.a)) / 4.0 > threshold;
+}
+
+static Color aa_average(Color c1, Color c2, Color c3, Color c4) {      /* antialiaser.rs:164-171 */
+  Color c = {(c1.r + c2.r + c3.r + c4.r) / 4.0, (c1.g + c2.g + c3.g + c4.g) / 4.0,
+             (c1.b + c2.b + c3.b + c4.b) / 4.0, (c1.a + c2.a + c3.a + c4.a) / 4.0};
+  return c;
+}
+
+static Color aa_sub(AaPixel *a, int sx, int sy) {                       /* antialiaser.rs:101-115 */
+  int i = sx * a->size + sy;
+  if (a->have[i]) return a->grid[i];
+  a->rays++;
+  Color c = get_pixel(a->sc, (double)a->x + ((double)sx / (double)a->size),
+                      (double)a->y + ((double)sy / (double)a->size));
+  a->grid[i] = c; a->have[i] = 1;
+  return c;
+}
+
+static Color aa_cell(AaPixel *a, int x1, int y1, int x2, int y2, int level) {   /* antialiaser.rs:124-152 */
+  Color c1 = aa_sub(a, x1, y1), c2 = aa_sub(a, x2, y1), c3 = aa_sub(a, x1, y2), c4 = aa_sub(a, x2, y2);
+  int different = aa_different(c1, c2, a->threshold) || aa_different(c1, c3, a->threshold) ||
+                  aa_different(c1, c4, a->threshold);
+  if (!different || level <= 0) return aa_average(c1, c2, c3, c4);
+  int mx = x1 + (x2 - x1) / 2, my = y1 + (y2 - y1) / 2;
+  Color d1 = aa_cell(a, x1, y1, mx, my, level - 1);
+  Color d2 = aa_cell(a, mx, y1, x2, my, level - 1);
+  Color d3 = aa_cell(a, x1, my, mx, y2, level - 1);
+  Color d4 = aa_cell(a, mx, my, x2, y2, level - 1);
+  return aa_average(d1, d2, d3, d4);
+}
+
+typedef struct {
+  const orc_scene *sc; const uint8_t *src; size_t stride; double threshold; int level;
+  int tid, nthreads; double *f64; uint8_t *u8; uint64_t rays;
+} AaJob;
+
+static void aa_put(AaJob *j, int x, int y, Color c) {
+  size_t o = ((size_t)y * (size_t)j->sc->width + (size_t)x) * 4;
+  if (j->f64) { j->f64[o] = c.r; j->f64[o + 1] = c.g; j->f64[o + 2] = c.b; j->f64[o + 3] = c.a; }
+  if (j->u8) { j->u8[o] = to_u8(c.r); j->u8[o + 1] = to_u8(c.g); j->u8[o + 2] = to_u8(c.b); j->u8[o + 3] = to_u8(c.a); }
+}
+
+static void *aa_job(void *vj) {
+  AaJob *j = (AaJob *)vj;
+  const int W = j->sc->width, H = j->sc->height;
+  AaPixel a;
+  memset(&a, 0, sizeof a);
+  a.sc = j->sc; a.src = j->src; a.stride = j->stride; a.threshold = j->threshold; a.level = j->level;
+  a.size = (1 << j->level) + 1;                                          /* antialiaser.rs:20 */
+  a.grid = (Color *)malloc(sizeof(Color) * (size_t)a.size * (size_t)a.size);
+  a.have = (unsigned char *)malloc((size_t)a.size * (size_t)a.size);
+  for (int y = 0; y < H; ++y) {
+    if (y % j->nthreads != j->tid) continue;
+    if (y == H - 1) {                  /* debug_window.rs:298: the AA pass never touches the last row */
+      for (int x = 0; x < W; ++x) aa_put(j, x, y, aa_src(&a, x, y));
+      continue;
+    }
+    for (int x = 0; x < W - 1; ++x) {                                    /* antialiaser.rs:53-71 */
+      const int n = a.size - 1;
+      memset(a.have, 0, (size_t)a.size * (size_t)a.size);                /* clear_matrices */
+      a.x = x; a.y = y;
+      a.grid[0] = aa_src(&a, x, y);                 a.have[0] = 1;        /* :96-99 */
+      a.grid[0 * a.size + n] = aa_src(&a, x, y + 1); a.have[0 * a.size + n] = 1;
+      a.grid[n * a.size + 0] = aa_src(&a, x + 1, y); a.have[n * a.size + 0] = 1;
+      a.grid[n * a.size + n] = aa_src(&a, x + 1, y + 1); a.have[n * a.size + n] = 1;
+      aa_put(j, x, y, aa_cell(&a, 0, 0, n, n, j->level));
+    }
+    aa_put(j, W - 1, y, aa_src(&a, W - 1, y));                          /* copy the last pixel */
+  }
+  j->rays = a.rays;
+  free(a.grid); free(a.have);
+  return NULL;
+}
+
+/* Anti-alias a whole quantised frame (RGBA8, row stride `stride` bytes) of the scene's size.
+ * Outputs (either may be NULL) are full frames; the last row and column are the source pixels
+ * re-quantised.  Returns the number of sub-pixel rays traced (the reference's ray_counter). */
+long long orc_antialias(const orc_scene *sc, const uint8_t *src, size_t stride, double threshold,
+                        int level, double *f64, uint8_t *u8, int nthreads) {
+  if (level < 0) level = 0;
+  if (level > 12) return -1;
+  if (nthreads < 1) nthreads = 1;
+  AaJob *jobs = (AaJob *)calloc((size_t)nthreads, sizeof(AaJob));
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int t = 0; t < nthreads; ++t) {
+    jobs[t].sc = sc; jobs[t].src = src; jobs[t].stride = stride; jobs[t].threshold = threshold;
+    jobs[t].level = level; jobs[t].tid = t; jobs[t].nthreads = nthreads; jobs[t].f64 = f64; jobs[t].u8 = u8;
+  }
+  if (nthreads == 1) aa_job(&jobs[0]);
+  else {
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, aa_job, &jobs[t]);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  }
+  long long rays = 0;
+  for (int t = 0; t < nthreads; ++t) rays += (long long)jobs[t].rays;
+  free(jobs); free(th);
+  return rays;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Orthogonal preview views (debug_window.rs:166-227, ray_debugger.rs:33-68). */
+/* ------------------------------------------------------------------------- */
+typedef struct { double distance; const RTObject *foremost, *cur; } OrthoCtx;
+static void add_ortho(void *vctx, double d) {                                      /* debug_window.rs:205-210 */
+  OrthoCtx *c = (OrthoCtx *)vctx;
+  if (d < c->distance) { c->foremost = c->cur; c->distance = d; }
+}
+
+static double *vaxis(Vec *v, int a) { return a == 0 ? &v->x : (a == 1 ? &v->y : &v->z); }
+
+/* Rows [y0, y1) of an orthogonal view at the scene's W x H: flat RTObject::get_color
+ * (rt_object.rs:45-47) of the object with the smallest intersection distance (any sign, no EPS),
+ * Color::EMPTY on a miss.  Returns -1 for invalid axes (the reference panics). */
+int orc_render_ortho(const orc_scene *sc, int axis1, int axis2, double dir1, double dir2, double scale,
+                     int y0, int y1, double *f64, uint8_t *u8) {
+  const int W = sc->width, H = sc->height;
+  const double center_x = (double)W / 2.0, center_y = (double)H / 2.0;
+  int axis3;
+  if (axis1 < 0 || axis1 > 2 || axis2 < 0 || axis2 > 2) return -1;
+  if (axis1 != 0 && axis2 != 0) axis3 = 0;
+  else if (axis1 != 1 && axis2 != 1) axis3 = 1;
+  else if (axis1 != 2 && axis2 != 2) axis3 = 2;
+  else return -1;                                                                  /* panic!("Invalid axes") */
+  Vec direction = {0.0, 0.0, 0.0};
+  *vaxis(&direction, axis3) = 1.0;
+  (void)H;
+  for (int y = y0; y < y1; ++y) {
+    for (int x = 0; x < W; ++x) {
+      Ray ray;
+      ray.point.x = ray.point.y = ray.point.z = 0.0;
+      *vaxis(&ray.point, axis1) = (((double)x - center_x) * dir1) / scale;
+      *vaxis(&ray.point, axis2) = (((double)y - center_y) * dir2) / scale;
+      *vaxis(&ray.point, axis3) = 10000.0;
+      ray.direction = direction;
+      OrthoCtx oc = {INFINITY, NULL, NULL};
+      for (int i = 0; i < sc->n_objects; ++i) {
+        oc.cur = &sc->objects[i];
+        rtobject_intersects(&sc->objects[i], ray, add_ortho, &oc);
+      }
+      Color c = {0.0, 0.0, 0.0, 0.0};                                              /* Color::EMPTY */
+      if (oc.foremost) {
+        const Material *m = &oc.foremost->material;
+        if (m->textured) { UV uv = {0.0, 0.0}; c = texture_color_at(m->texture, uv); }
+        else c = m->color;
+      }
+      size_t o = ((size_t)(y - y0) * (size_t)W + (size_t)x) * 4;
+      if (f64) { f64[o] = c.r; f64[o + 1] = c.g; f64[o + 2] = c.b; f64[o + 3] = c.a; }
+      if (u8) { u8[o] = to_u8(c.r); u8[o + 1] = to_u8(c.g); u8[o + 2] = to_u8(c.b); u8[o + 3] = to_u8(c.a); }
+    }
+  }
+  return 0;
+}
+
+/* RayDebugger::record_rays (ray_debugger.rs:92-137): the rays of pixel (x, y) in callback order.
+ * Returns the number of rays (records beyond cap are dropped); rgba = get_pixel's colour. */
+int orc_record_rays(const orc_scene *sc, double x, double y, OrcRayRecord *out, int cap, double rgba[4]) {
+  OrcRec r = {sc, out, cap, 0};
+  g_rec = &r;
+  Color c = get_pixel(sc, x, y);
+  g_rec = NULL;
+  rgba[0] = c.r; rgba[1] = c.g; rgba[2] = c.b; rgba[3] = c.a;
+  return r.n;
+}
+int orc_ray_record_size(void) { return (int)sizeof(OrcRayRecord); }

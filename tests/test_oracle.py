@@ -126,3 +126,23 @@ def test_flop_fixture_consistent():
             assert sum(d["row_flops"]) == d["totals"]["flop"]
             assert len(d["row_flops"]) == d["height"]
             assert d["totals"]["ray_primary"] == d["width"] * d["height"]
+
+
+@pytest.mark.parametrize("name,time,W,H,threshold,level", [
+    ("globes", 0.0, 24, 18, 0.01, 3), ("globes", 0.3, 20, 16, 0.05, 2), ("spinning_globes", 0.2, 16, 12, 0.01, 3),
+])
+def test_antialias_pyref_bit_equal(worldmap, name, time, W, H, threshold, level):
+    """Adaptive anti-aliasing (antialiaser.rs): both restatements agree bit for bit, including the
+    number of sub-pixel rays traced (the reference's ray_counter)."""
+    from oracle import oracle as O
+    from oracle import pyref as P
+    text = scene_text(name)
+    ref = O.OracleScene(text, time, W, H)
+    _, u8 = ref.render()
+    f, a8, rays = ref.antialias(u8, threshold, level)
+    py = P.Scene(text, time, W, H, {"worldmap.png": P.load_texture(worldmap)})
+    rows, prays = P.antialias(py, [[tuple(int(v) for v in px) for px in row] for row in u8], threshold, level)
+    pf = np.array([[[c.r, c.g, c.b, c.a] for c in row] for row in rows])
+    assert rays == prays and rays > 0
+    assert np.array_equal(pf, f)
+    assert np.array_equal(a8[-1], u8[-1]) and np.array_equal(a8[:, -1], u8[:, -1])

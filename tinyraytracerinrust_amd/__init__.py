@@ -8,6 +8,11 @@ this Python layer mirrors the reference's RayTracer interface over that ABI.
 from ._lib import RtError, lib  # noqa: F401
 from .raytracer import (  # noqa: F401
     MAX_FRAMES,
+    ORTHO_SCALE,
+    AntiAliaser,
+    OrthoAxes,
+    RAY_RECORD_DTYPE,
+    RayDebugger,
     MatrixTransformation,
     RayTracer,
     Renderer,
@@ -21,7 +26,7 @@ from .raytracer import (  # noqa: F401
 )
 
 __all__ = [
-    "RtError", "lib", "MAX_FRAMES", "MatrixTransformation", "RayTracer", "Renderer", "Scene",
+    "RtError", "lib", "MAX_FRAMES", "ORTHO_SCALE", "AntiAliaser", "OrthoAxes", "RAY_RECORD_DTYPE", "RayDebugger", "MatrixTransformation", "RayTracer", "Renderer", "Scene",
     "TransformationStack", "device_count", "read_png_rgba8", "solid_material", "textured_material",
     "write_png",
 ]

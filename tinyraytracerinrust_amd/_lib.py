@@ -80,6 +80,12 @@ SIGNATURES = {
     "rt_render_row_bands": (_I, [_P, _U32, _U32, _U32, _U32, ctypes.c_int32, _P, ctypes.c_size_t, _P]),
     "rt_render_rows_f64": (_I, [_P, _U32, _U32, ctypes.c_int32, _P, ctypes.c_size_t, _P]),
     "rt_render_points_f64": (_I, [_P, _P, ctypes.c_size_t, ctypes.c_int32, _P, _P]),
+    "rt_record_rays": (_I, [_P, ctypes.c_double, ctypes.c_double, ctypes.c_int32, _P, ctypes.c_int32,
+                            ctypes.POINTER(ctypes.c_int32), _P]),
+    "rt_render_ortho": (_I, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                             ctypes.c_uint32, ctypes.c_uint32, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P]),
+    "rt_antialias": (_I, [_P, _P, ctypes.c_size_t, ctypes.c_double, ctypes.c_int32, ctypes.c_int32, _P,
+                          ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64), _P]),
     "rt_ctx_last_kernel_ms": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
     "rt_ctx_synchronize": (_I, [_P]),
     "rt_ctx_free": (None, [_P]),

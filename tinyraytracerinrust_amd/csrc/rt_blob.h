@@ -84,6 +84,7 @@ struct alignas(16) RtObject {
   int32_t shadow_skip;              // transparency == 1.0: shadow multiplies by 1 -> no-op
   int32_t cull;                     // RtCull for the object box (hull of its leaves' boxes)
   double color[3];                  // material colour (solid)
+  double color_a;                   // its alpha (only the ortho views read it)
   double reflectivity, transparency;
   double blo[3], bhi[3];
   int32_t leaf_cull;                // 1: per-leaf boxes are tighter than the object box

@@ -367,7 +367,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
     ob.textured = m.texture >= 0;
     ob.tex = m.texture >= 0 ? m.texture : 0;
     if (m.texture >= (int32_t)s.textures.size()) return fail(RT_ERR_INVALID, "bad texture id %d", m.texture);
-    ob.color[0] = m.color[0]; ob.color[1] = m.color[1]; ob.color[2] = m.color[2];
+    ob.color[0] = m.color[0]; ob.color[1] = m.color[1]; ob.color[2] = m.color[2]; ob.color_a = m.color[3];
     ob.reflectivity = m.reflectivity;
     ob.transparency = m.transparency;
     ob.shadow_skip = m.transparency == 1.0;

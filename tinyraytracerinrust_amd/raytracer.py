@@ -221,6 +221,51 @@ class Renderer:
                                          ctypes.c_void_p(out.ctypes.data), None))
         return out
 
+    def antialias(self, frame, threshold: float = 0.01, level: int = 3, max_depth: int = -1, f64: bool = False,
+                  out=None, stream=None):
+        """rt_antialias over a whole quantised frame.  ``frame`` is an (H, W, 4) uint8 torch tensor
+        on this device (returns a device tensor; asynchronous up to the edge count) or a numpy
+        array (returns numpy).  Returns (anti-aliased frame, sub-pixel rays traced); the frame is
+        float64 RGBA with ``f64``."""
+        rays = ctypes.c_uint64(0)
+        if isinstance(frame, np.ndarray):
+            src = np.ascontiguousarray(frame, dtype=np.uint8)
+            res = out if out is not None else np.empty(src.shape, np.float64 if f64 else np.uint8)
+            sp, ss, rp, rs = src.ctypes.data, src.strides[0], res.ctypes.data, res.strides[0]
+            st = 0
+        else:
+            import torch
+            src = frame
+            res = out if out is not None else torch.empty(tuple(frame.shape), dtype=torch.float64 if f64 else torch.uint8,
+                                                          device=frame.device)
+            sp, ss = src.data_ptr(), src.stride(0) * src.element_size()
+            rp, rs = res.data_ptr(), res.stride(0) * res.element_size()
+            st = (stream if stream is not None else torch.cuda.current_stream(frame.device)).cuda_stream
+        u8p, u8s, fp, fs = (None, 0, rp, rs) if f64 else (rp, rs, None, 0)
+        check(lib().rt_antialias(self.h, ctypes.c_void_p(sp), ss, float(threshold), int(level), int(max_depth),
+                                 ctypes.c_void_p(u8p), u8s, ctypes.c_void_p(fp), fs, ctypes.byref(rays),
+                                 ctypes.c_void_p(st)))
+        return res, rays.value
+
+    def record_rays(self, x: float, y: float, max_depth: int = -1, cap: int = 1 << 17):
+        """rt_record_rays: (records as a RAY_RECORD_DTYPE array in callback order, pixel colour)."""
+        buf = np.zeros(cap, RAY_RECORD_DTYPE)
+        n = ctypes.c_int32(0)
+        rgba = (ctypes.c_double * 4)()
+        check(lib().rt_record_rays(self.h, float(x), float(y), int(max_depth), ctypes.c_void_p(buf.ctypes.data),
+                                   cap, ctypes.byref(n), rgba))
+        return buf[:min(n.value, cap)].copy(), np.array(rgba[:])
+
+    def render_ortho(self, axes: "OrthoAxes", y0: int = 0, y1: Optional[int] = None, f64: bool = False) -> np.ndarray:
+        """rt_render_ortho rows [y0, y1) into a host array (uint8 RGBA, or float64 with ``f64``)."""
+        y1 = self.height if y1 is None else y1
+        out = np.empty((y1 - y0, self.width, 4), np.float64 if f64 else np.uint8)
+        p8, s8, pf, sf = (None, 0, out.ctypes.data, out.strides[0]) if f64 else (out.ctypes.data, out.strides[0], None, 0)
+        check(lib().rt_render_ortho(self.h, axes.axis1, axes.axis2, float(axes.dir1), float(axes.dir2),
+                                    float(axes.scale), y0, y1, ctypes.c_void_p(p8), s8, ctypes.c_void_p(pf), sf,
+                                    None))
+        return out
+
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()
         check(lib().rt_ctx_last_kernel_ms(self.h, ctypes.byref(ms)))
@@ -343,6 +388,92 @@ class RayTracer:
     def render_frame(self) -> np.ndarray:
         """The whole frame as RGBA8 (H, W, 4), quantised as easy_pixbuf.rs:46-53."""
         return self.renderer.render_rows_host(0, self.height)
+
+    def render_orthogonal_view_line(self, y: int, ortho_axes: "OrthoAxes") -> np.ndarray:
+        """DebugWindow::render_orthogonal_view_line (debug_window.rs:166-227): (W, 4) f64 colours."""
+        return _ortho_line(self, y, ortho_axes)
+
+    def render_orthogonal_view(self, area: str = "top") -> np.ndarray:
+        """A whole orthogonal preview ("top", "front", "side") as RGBA8 (H, W, 4)."""
+        return self.renderer.render_ortho(OrthoAxes.from_area(area))
+
+
+ORTHO_SCALE = 2.0   # ray_debugger.rs:11
+
+# rt_ray_record (include/rt_abi.h) as a numpy dtype
+RAY_RECORD_DTYPE = np.dtype([
+    ("depth", "<i4"), ("ray_type", "<i4"), ("object", "<i4"), ("intersected", "<i4"), ("has_normal", "<i4"),
+    ("pad", "<i4"), ("point", "<f8", 3), ("direction", "<f8", 3), ("distance", "<f8"),
+    ("intersection", "<f8", 3), ("normal", "<f8", 3), ("color", "<f8", 4)])
+RAY_TYPES = ("NormalRay", "ReflectionRay", "TransmissionRay")
+
+
+class RayDebugger:
+    """ray_debugger.rs:71-137: records every ray of one pixel (RayInfo list in callback order)."""
+
+    def __init__(self, width: int, height: int):
+        self.rays = np.zeros(0, RAY_RECORD_DTYPE)
+        self.debugged_position = None
+        self.width, self.height = width, height
+        self.show_normals = True
+
+    def record_rays(self, ray_tracer: "RayTracer", x: float, y: float) -> None:
+        if self.debugged_position == (x, y):          # already showing these rays (:93-97)
+            return
+        self.debugged_position = (x, y)
+        self.rays = ray_tracer.renderer.record_rays(x, y, ray_tracer.max_depth)[0]
+
+    def reset_debugger(self) -> None:
+        self.debugged_position = None
+
+
+class OrthoAxes:
+    """ray_debugger.rs:24-68: the axes of an orthogonal preview view."""
+
+    def __init__(self, axis1: int, axis2: int, dir1: float, dir2: float, scale: float = ORTHO_SCALE):
+        self.axis1, self.axis2, self.dir1, self.dir2, self.scale = int(axis1), int(axis2), dir1, dir2, scale
+
+    @staticmethod
+    def from_area(area: str) -> "OrthoAxes":
+        """impl From<DrawingArea> for OrthoAxes: "top", "front" or "side"."""
+        if area == "top":
+            return OrthoAxes(0, 2, 1.0, -1.0)
+        if area == "front":
+            return OrthoAxes(0, 1, 1.0, -1.0)
+        if area == "side":
+            return OrthoAxes(2, 1, -1.0, -1.0)
+        raise ValueError("Main view is not an orthogonal view!" if area == "main" else f"unknown area {area!r}")
+
+
+class AntiAliaser:
+    """antialiaser.rs:7-192: adaptive anti-aliasing of a rendered (quantised) frame.
+
+    ``AntiAliaser(ray_tracer, threshold=None, level=None)`` takes the reference's defaults
+    (0.1 and 3, antialiaser.rs:18-19); the GUI passes ANTIALIAS_THRESHOLD = 0.01 and
+    ANTIALIAS_LEVEL = 3 (debug_window.rs:26-27).  The whole frame is one GPU pass (rt_antialias);
+    ``ray_counter`` accumulates the sub-pixel rays traced like the reference's counter."""
+
+    def __init__(self, ray_tracer: "RayTracer", threshold: Optional[float] = None, level: Optional[int] = None):
+        self.ray_tracer = ray_tracer
+        self.threshold = 0.1 if threshold is None else float(threshold)
+        self.level = 3 if level is None else int(level)
+        self.size = (1 << self.level) + 1
+        self.ray_counter = 0
+
+    def set_threshold(self, threshold: float) -> None:
+        self.threshold = float(threshold)
+
+    def anti_alias_frame(self, frame, f64: bool = False):
+        """Every line of ``anti_alias_line_vec`` (antialiaser.rs:53-71) for y in 0..H-1, as the
+        AA worker does (debug_window.rs:298-318); the last row is passed through."""
+        out, rays = self.ray_tracer.renderer.antialias(frame, self.threshold, self.level, self.ray_tracer.max_depth,
+                                                       f64=f64)
+        self.ray_counter += rays
+        return out
+
+
+def _ortho_line(rt: "RayTracer", y: int, ortho_axes: OrthoAxes) -> np.ndarray:
+    return rt.renderer.render_ortho(ortho_axes, y, y + 1, f64=True)[0]
 
 
 def write_png(path: str, rgba8: np.ndarray, channels: int = 3) -> None:
