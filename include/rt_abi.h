@@ -128,6 +128,10 @@ int rt_scene_info(const rt_scene* scene, int32_t* n_objects, int32_t* n_lights, 
 /* Introspection (tests, debuggers): the camera as PerspectiveCamera::new builds it
  * (camera.rs:30-54): out = center[3], direction[3], right[3], up[3], aspect_ratio. */
 int rt_scene_get_camera(const rt_scene* scene, double out[13]);
+/* The device traversal order (tests): the object hierarchy the kernels walk, as n nodes in
+ * pre-order, node i = (obj[i], skip[i]); obj = -1 for a group node, skip = index after the
+ * node's subtree.  Object nodes appear in draw order.  Writes min(n, cap) nodes; *n = total. */
+int rt_scene_traversal(const rt_scene* scene, int32_t* obj, int32_t* skip, int32_t cap, int32_t* n);
 /* Light i: point[3] (world space, as stored by add_light) and color[4]. */
 int rt_scene_get_light(const rt_scene* scene, int32_t i, double point[3], double color[4]);
 void rt_scene_free(rt_scene* scene);

@@ -74,6 +74,23 @@ def test_scene_parity(T, worldmap, name, time, W, H, depth):
     assert_close(gu, gf, ru, rf, f"{name} t={time} {W}x{H} d={depth}")
 
 
+EDGE_SCENES = {
+    # a wall beyond the culling range (|coords| > 1e6): boxes never culled, never grouped
+    "huge_wall": "draw(sphere(<0, 0, 2000000>, 1999000, red * 0.8, 0.3))\n"
+                 "draw(sphere(<0, 0, 0>, 20, red, 0.5))\ndraw(cube(<25, -10, 0>, 10, red * 0.5, 0.2))",
+    # translation-only inverses with -0 entries: the diagonal-affine transform short form
+    "signed_zero_xf": "translate(0, 5, 0) draw(sphere(<0, 0, 0>, 30, red, 0.3))\n"
+                      "translate(0, -30, 0) draw(cube(<0, 0, 0>, 20, red * 0.5, 0.5))\n"
+                      "scale(1, 0.5, 1) draw(sphere(<30, 0, 0>, 10, red * 0.2, 0.4, 0.5))",
+}
+
+
+@pytest.mark.parametrize("name", sorted(EDGE_SCENES))
+def test_edge_scene_parity(T, name):
+    gu, gf, ru, rf = render_pair(T, EDGE_SCENES[name], 0.0, 160, 120, 10)
+    assert_close(gu, gf, ru, rf, name)
+
+
 def test_single_sphere_primary_only(T):
     """BASELINE config 2 at reduced size: draw(sphere(<0,0,0>, 30, red)), max_depth 0."""
     text = "draw(sphere(<0, 0, 0>, 30, red))"

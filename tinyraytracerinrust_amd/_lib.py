@@ -67,6 +67,8 @@ SIGNATURES = {
     "rt_scene_set_max_depth": (_I, [_P, ctypes.c_int32]),
     "rt_scene_compile": (_I, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_double, _U32, _U32,
                               ctypes.POINTER(_P)]),
+    "rt_scene_traversal": (_I, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
+                                ctypes.POINTER(ctypes.c_int32)]),
     "rt_scene_info": (_I, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_U32),
                            ctypes.POINTER(_U32)]),

@@ -45,6 +45,27 @@ __device__ unsigned long long g_rt_prof[8];
 #define PROF_ADD(sec, v) (void)0
 #endif
 
+// Diagnostic event-count build (make diag NAME=cnt DIAG=-DRT_COUNT; never the product): per ray
+// category (0 primary, 1 secondary, 2 shadow) rays, object box tests, objects entered, leaf box
+// tests, leaf evaluations (all / sphere / plane / cube), CSG filter calls; lane-events, one atomic
+// per wave per event.
+#ifdef RT_COUNT
+__device__ unsigned long long g_rt_cnt[32];
+#define CNT(i)                                                                          \
+  do {                                                                                  \
+    const unsigned long long m_ = __ballot(1);                                          \
+    if ((int)__lane_id() == __ffsll((long long)m_) - 1) atomicAdd(&g_rt_cnt[i], (unsigned long long)__popcll(m_)); \
+  } while (0)
+#define CNTW(i)                                                                         \
+  do {                                                                                  \
+    const unsigned long long m_ = __ballot(1);                                          \
+    if ((int)__lane_id() == __ffsll((long long)m_) - 1) atomicAdd(&g_rt_cnt[i], 1ull); \
+  } while (0)
+#else
+#define CNT(i) (void)0
+#define CNTW(i) (void)0
+#endif
+
 namespace {
 
 // Scene tables are read-only for the whole launch: view them through the CONSTANT address space
@@ -55,13 +76,14 @@ template <class T> __device__ __forceinline__ cptr<T> as_const(const T* p) { ret
 
 struct DS {                         // device view of RtDevScene
   cptr<RtObject> objects;
+  cptr<RtTrav> trav;
   cptr<RtNode> nodes;
   cptr<RtLeaf> leaves;
   cptr<RtProg> prog;
   cptr<RtLight> lights;
   cptr<RtTexture> textures;
   const uint8_t* texels;            // per-lane texel gathers stay global (vector) loads
-  int n_objects, n_lights;
+  int n_objects, n_lights, n_trav;
   int shadow_early_out;
 };
 
@@ -85,6 +107,21 @@ template <class P> __device__ __forceinline__ V3 xf(P m, V3 v) {
           m[4] * v.x + m[5] * v.y + m[6] * v.z + m[7],
           m[8] * v.x + m[9] * v.y + m[10] * v.z + m[11]};
 }
+// transform_vector by a diagonal-affine matrix (RtLeaf::xdiag): bit-identical to xf() for finite
+// inputs (rt_blob.h), 6 flops instead of 18.
+template <class P> __device__ __forceinline__ V3 xf_diag(P m, V3 v) {
+  return {m[0] * v.x + m[3], m[5] * v.y + m[7], m[10] * v.z + m[11]};
+}
+__device__ __forceinline__ bool finite3(V3 v) { return isfinite(v.x) && isfinite(v.y) && isfinite(v.z); }
+// Is every active lane's vector finite?  Wave-uniform, so the short transform is a scalar branch.
+__device__ __forceinline__ bool wave_finite(V3 a) { return __ballot(!finite3(a)) == 0; }
+__device__ __forceinline__ bool wave_finite(V3 a, V3 b) { return __ballot(!(finite3(a) && finite3(b))) == 0; }
+// The leaf's inverse transform of a point (transformation.rs:53-59); `fin` = wave_finite(v).
+__device__ __forceinline__ V3 leaf_inv_xf(cptr<RtLeaf> L, V3 v, bool fin) {
+  if (L->xdiag && fin) return xf_diag(L->inv, v);
+  return xf(L->inv, v);
+}
+
 // color.rs:36-53: clamp each channel (NaN passes through)
 __device__ __forceinline__ double in_limit(double x) { return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x); }
 __device__ __forceinline__ Col in_range(double r, double g, double b) { return {in_limit(r), in_limit(g), in_limit(b)}; }
@@ -104,17 +141,17 @@ template <class P> __device__ __forceinline__ bool on_plane(P pl, V3 q) {       
   return fabs(pl[0] * q.x + pl[1] * q.y + pl[2] * q.z + pl[3]) < EPS;
 }
 
-__device__ bool leaf_inside(cptr<RtLeaf> L, V3 p) {
+__device__ bool leaf_inside(cptr<RtLeaf> L, V3 p, bool fin) {
   int k = L->kind;
   if (k == RT_N_PLANE) return false;                                        // :186-188
-  V3 q = xf(L->inv, p);
+  V3 q = leaf_inv_xf(L, p, fin);
   if (k == RT_N_SPHERE) return len(sub(q, ld3(L->c))) <= L->r_eps;         // :70-74
   return q.x <= L->hi[0] && q.x >= L->lo[0] && q.y <= L->hi[1] &&          // :319-328
          q.y >= L->lo[1] && q.z <= L->hi[2] && q.z >= L->lo[2];
 }
 
-__device__ bool leaf_on_surface(cptr<RtLeaf> L, V3 p) {
-  V3 q = xf(L->inv, p);
+__device__ bool leaf_on_surface(cptr<RtLeaf> L, V3 p, bool fin) {
+  V3 q = leaf_inv_xf(L, p, fin);
   int k = L->kind;
   if (k == RT_N_SPHERE) return fabs(len(sub(q, ld3(L->c))) - L->radius) < EPS;   // :76-80
   if (k == RT_N_PLANE) return on_plane(L->pl[0], q);                            // :190-194
@@ -127,10 +164,10 @@ __device__ bool leaf_on_surface(cptr<RtLeaf> L, V3 p) {
   return false;
 }
 
-__device__ V3 leaf_normal(cptr<RtLeaf> L, V3 p) {
+__device__ V3 leaf_normal(cptr<RtLeaf> L, V3 p, bool fin) {
   int k = L->kind;
   if (k == RT_N_PLANE) return ld3(L->pn[0]);                               // :182-184
-  V3 q = xf(L->inv, p);
+  V3 q = leaf_inv_xf(L, p, fin);
   if (k == RT_N_SPHERE) {                                                  // :64-68
     V3 n = sub(q, ld3(L->c));
     return normalized(sub(xf(L->mat, n), ld3(L->mat_o)));
@@ -142,7 +179,7 @@ __device__ V3 leaf_normal(cptr<RtLeaf> L, V3 p) {
 
 // MathSphere::get_uv_coordinates (:82-114): the centre is subtracted BEFORE the inverse transform
 __device__ void sphere_uv(cptr<RtLeaf> L, V3 p, double* u, double* v) {
-  V3 q = xf(L->inv, sub(p, ld3(L->c)));
+  V3 q = xf(L->inv, sub(p, ld3(L->c)));           // per shaded hit only: no short form
   q = scale(normalized(q), 1.0 - EPS);
   double phi = rt_acos(-((0.0 * q.x + 1.0 * q.y) + 0.0 * q.z));             // up = (0,1,0)
   if (isnan(phi)) phi = 0.0;
@@ -154,9 +191,16 @@ __device__ void sphere_uv(cptr<RtLeaf> L, V3 p, double* u, double* v) {
 
 // Candidate hit distances of one primitive for the world ray (ro, rd):
 // RTObject::intersects (rt_object.rs:28-31) = reverse_transform_ray + MathShape::intersects.
-__device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, double* t0, double* t1) {
-  V3 o = xf(L->inv, ro);                                                   // transformation.rs:88-93
-  V3 d = sub(xf(L->inv, rd), ld3(L->inv_o));
+// `fin` = wave_finite(ro, rd): selects the exact short form for diagonal-affine leaves.
+__device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, bool fin, double* t0, double* t1) {
+  V3 o, d;
+  if (L->xdiag && fin) {                                                   // transformation.rs:88-93
+    o = xf_diag(L->inv, ro);
+    d = sub(xf_diag(L->inv, rd), ld3(L->inv_o));
+  } else {
+    o = xf(L->inv, ro);
+    d = sub(xf(L->inv, rd), ld3(L->inv_o));
+  }
   int k = L->kind;
   if (k == RT_N_SPHERE) {                                                  // math_shapes.rs:42-62
     V3 v = sub(o, ld3(L->c));
@@ -202,12 +246,13 @@ __device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, dou
 // Conjunction of every CSG ancestor's sibling test for a hit of leaf L at world point p
 // (csg.rs:43-95), as a postfix program over a bit stack.
 __device__ bool leaf_filter(const DS& S, cptr<RtLeaf> L, V3 p) {
+  const bool fin = wave_finite(p);
   uint32_t st = 0;
   const int e = L->prog_end;
   for (int k = L->prog_begin; k < e; ++k) {
     const int op = S.prog[k].op, arg = S.prog[k].arg;
     if (op == RT_OP_INSIDE) {
-      st = (st << 1) | (leaf_inside(&S.leaves[arg], p) ? 1u : 0u);
+      st = (st << 1) | (leaf_inside(&S.leaves[arg], p, fin) ? 1u : 0u);
     } else if (op == RT_OP_REQUIRE) {
       uint32_t v = st & 1u;
       st >>= 1;
@@ -226,85 +271,91 @@ __device__ bool leaf_filter(const DS& S, cptr<RtLeaf> L, V3 p) {
 }
 
 // ------------------------------------------------------------------ conservative culling
-// Does the ray segment t in [0, tmax] come near the box?  Only ever answers "no" when no point of
-// the segment is inside [lo, hi]; boxes are inflated on the host (scene.cpp leaf_box) and tmax
-// carries a relative margin, so f64 rounding here cannot cull a hit the exact code would accept.
-// NaN anywhere makes the comparisons false and the answer "yes" (evaluate exactly).
-template <class P> __device__ __forceinline__ bool box_may_hit(P lo, P hi, V3 o, V3 d, V3 inv, double tmax) {
-#ifndef RT_BRANCHY_BOX
-  // Select form (no exec-mask branches).  An axis with d == 0 only asks whether the origin lies
-  // in the slab; otherwise the usual interval narrowing, where a NaN bound narrows nothing.
-  double tn = 0.0, tf = tmax;
-  bool out = false;
-#define RT_BOXAX(P, D, I, IV)                                                   \
-  {                                                                             \
-    const double a = (lo[I] - P) * IV, b = (hi[I] - P) * IV;                    \
-    const bool z = D == 0.0;                                                    \
-    out = out || (z && (P < lo[I] || P > hi[I]));                               \
-    const bool sw = a > b;                                                      \
-    const double mn = sw ? b : a, mx = sw ? a : b;                              \
-    tn = (!z && mn > tn) ? mn : tn;                                             \
-    tf = (!z && mx < tf) ? mx : tf;                                             \
-  }
-  RT_BOXAX(o.x, d.x, 0, inv.x)
-  RT_BOXAX(o.y, d.y, 1, inv.y)
-  RT_BOXAX(o.z, d.z, 2, inv.z)
-#undef RT_BOXAX
-  return !out && !(tn > tf);
-#else
-  double tn = 0.0, tf = tmax;
-#define RT_BOXAX(P, D, I, IV)                                                   \
-  if (D == 0.0) {                                                               \
-    if (P < lo[I] || P > hi[I]) return false;                                   \
-  } else {                                                                      \
-    double a = (lo[I] - P) * IV, b = (hi[I] - P) * IV;                          \
-    if (a > b) { double tmp = a; a = b; b = tmp; }                              \
-    if (a > tn) tn = a;                                                         \
-    if (b < tf) tf = b;                                                         \
-  }
-  RT_BOXAX(o.x, d.x, 0, inv.x)
-  RT_BOXAX(o.y, d.y, 1, inv.y)
-  RT_BOXAX(o.z, d.z, 2, inv.z)
-#undef RT_BOXAX
-  return !(tn > tf);
-#endif
-}
+// Does the ray segment t in [0, tmax] come near the box?  Only ever answers "no" when no point
+// where an accepted hit could lie is on the segment.  Per axis the slab times are
+// (bound - o) * inv with inv ~ 1/d to ~1e-15: for |origin|, |bounds| <= 1e6 the error in
+// space is < 1e-9, far inside the 1e-6 inflation of every box (scene.cpp leaf_box), so each
+// axis interval computed still contains the parameter of any point of the un-inflated region;
+// tmax carries a 1e-7 relative margin on top.  min/max are IEEE minNum/maxNum: a NaN slab time
+// narrows nothing, and a ray outside the proven range (cull_ray) gets NaN inv -> never culled.
+struct CullRay { V3 inv, o; };
+
 // Reciprocal for the culling slabs only (never for a value the reference computes): hardware
-// rcp + one Newton step, ~1e-15 relative -- far inside the culling margins.  d == 0 -> NaN or
-// inf, which box_may_hit never reads (that axis takes the d == 0 branch).
+// rcp + one Newton step.  d == 0 (or |d| < 1e-200) -> +-1e200, which makes the slab test the
+// "origin inside the slab" check while every product stays finite.
 __device__ __forceinline__ double cull_rcp(double x) {
-#ifdef RT_EXACT_CULL_RCP
-  return 1.0 / x;
-#else
   const double r = __builtin_amdgcn_rcp(x);
-  return fma(r, fma(-x, r, 1.0), r);
-#endif
+  const double n = fma(r, fma(-x, r, 1.0), r);
+  return fabs(x) < 1e-200 ? copysign(1e200, x) : n;
 }
-__device__ __forceinline__ V3 cull_inv(V3 d) { return {cull_rcp(d.x), cull_rcp(d.y), cull_rcp(d.z)}; }
+__device__ __forceinline__ CullRay cull_ray(V3 o, V3 d) {
+  const double ad = fmax(fmax(fabs(d.x), fabs(d.y)), fabs(d.z));
+  const bool ok = fabs(o.x) <= RT_CULL_COORD_MAX && fabs(o.y) <= RT_CULL_COORD_MAX && fabs(o.z) <= RT_CULL_COORD_MAX &&
+                  ad >= 1e-100 && ad <= 1e100;
+  const double nan = __builtin_nan("");
+  const V3 inv = ok ? V3{cull_rcp(d.x), cull_rcp(d.y), cull_rcp(d.z)} : V3{nan, nan, nan};
+  return {inv, o};
+}
+// (bound - o) * inv per slab: measured faster than fma(bound, inv, -o*inv), which keeps three
+// more doubles live across the traversal (profiles/r01n_variant_timing.txt).
+template <class P> __device__ __forceinline__ bool box_may_hit(P lo, P hi, const CullRay& r, double tmax) {
+  const double ax = (lo[0] - r.o.x) * r.inv.x, bx = (hi[0] - r.o.x) * r.inv.x;
+  const double ay = (lo[1] - r.o.y) * r.inv.y, by = (hi[1] - r.o.y) * r.inv.y;
+  const double az = (lo[2] - r.o.z) * r.inv.z, bz = (hi[2] - r.o.z) * r.inv.z;
+  const double tn = fmax(fmax(fmin(ax, bx), fmin(ay, by)), fmax(fmin(az, bz), 0.0));
+  const double tf = fmin(fmin(fmax(ax, bx), fmax(ay, by)), fmin(fmax(az, bz), tmax));
+  return !(tn > tf);
+}
 __device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) + 1e-7; }
 
 // ------------------------------------------------------------------ traversal (raytracer.rs)
+// Both traversals walk the object hierarchy (RtTrav, pre-order over contiguous draw-order runs)
+// wave-coherently: `i` is uniform, a lane that misses a group resumes at its skip index, and the
+// wave jumps over a group no lane entered.  Objects are visited in draw order either way.
+
 // Nearest hit over all objects in draw order: accept d if d > EPS && d < nearest
 // (raytracer.rs:141-150).  The acceptance test is pure, so it runs BEFORE the (pure) CSG
 // filter: candidates that cannot win never pay for the sibling is_inside tests.
-__device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist) {
+__device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0) {
+  [[maybe_unused]] const int cb = cat * 9;
+  CNT(cb + 0);
   double best = INFINITY;
   int bobj = -1;
-  const V3 inv = cull_inv(rd);
-  for (int o = 0; o < S.n_objects; ++o) {
+  const CullRay cr = cull_ray(ro, rd);
+  const bool fin = wave_finite(ro, rd);
+  int resume = 0;
+  for (int i = 0; i < S.n_trav;) {
+    cptr<RtTrav> T = &S.trav[i];
+    const bool act = i >= resume;
+    if (T->obj < 0) {                                    // group node
+      CNT(28 + cat);
+      const bool in = act && box_may_hit(T->blo, T->bhi, cr, cull_tmax(best));
+      if (act && !in) resume = T->skip;
+      i = __ballot(in) ? i + 1 : T->skip;
+      continue;
+    }
+    ++i;
+    if (!act) continue;
+    const int o = T->obj;
     cptr<RtObject> O = &S.objects[o];
     if (O->cull == RT_CULL_ALWAYS) continue;
-    if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, ro, rd, inv, cull_tmax(best))) continue;
+    if (O->cull == RT_CULL_BOX) CNT(cb + 1);
+    if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, cr, cull_tmax(best))) continue;
+    CNT(cb + 2);
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
     for (int l = lb; l < le; ++l) {
       cptr<RtLeaf> L = &S.leaves[l];
       if (O->leaf_cull) {
         if (L->cull == RT_CULL_ALWAYS) continue;
-        if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, ro, rd, inv, cull_tmax(best))) continue;
+        if (L->cull == RT_CULL_BOX) CNT(cb + 3);
+        if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, cull_tmax(best))) continue;
       }
+      CNT(cb + 4);
+      CNT(cb + 5 + (L->kind == RT_N_SPHERE ? 0 : L->kind == RT_N_PLANE ? 1 : 2));
       double t0 = 0.0, t1 = 0.0;
-      int n = leaf_candidates(L, ro, rd, &t0, &t1);
+      int n = leaf_candidates(L, ro, rd, fin, &t0, &t1);
       const bool filtered = L->prog_end != L->prog_begin;
+      if (filtered && ((n >= 1 && t0 > EPS && t0 < best) || (n >= 2 && t1 > EPS))) CNT(cb + 8);
       if (n >= 1 && t0 > EPS && t0 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) {
         best = t0; bobj = o;
       }
@@ -321,24 +372,45 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist) {
 // Early-out once the product is exactly 0 (it stays 0: every factor is finite, checked on the
 // host), objects of transparency exactly 1.0 are skipped (x * 1.0 == x).
 __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
+  [[maybe_unused]] constexpr int cb = 18;
+  CNT(cb + 0);
   double tr = 1.0;
-  const V3 inv = cull_inv(dir);
+  const CullRay cr = cull_ray(p, dir);
+  const bool fin = wave_finite(p, dir);
   const double tmax = cull_tmax(dist);
-  for (int o = 0; o < S.n_objects; ++o) {
-    cptr<RtObject> O = &S.objects[o];
+  int resume = 0;
+  for (int i = 0; i < S.n_trav;) {
+    cptr<RtTrav> T = &S.trav[i];
+    const bool act = i >= resume;
+    if (T->obj < 0) {                                    // group node
+      CNT(30);
+      const bool in = act && box_may_hit(T->blo, T->bhi, cr, tmax);
+      if (act && !in) resume = T->skip;
+      i = __ballot(in) ? i + 1 : T->skip;
+      continue;
+    }
+    ++i;
+    if (!act) continue;
+    cptr<RtObject> O = &S.objects[T->obj];
     if (O->shadow_skip || O->cull == RT_CULL_ALWAYS) continue;
-    if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, p, dir, inv, tmax)) continue;
+    if (O->cull == RT_CULL_BOX) CNT(cb + 1);
+    if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, cr, tmax)) continue;
+    CNT(cb + 2);
     const double tobj = O->transparency;
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
     for (int l = lb; l < le; ++l) {
       cptr<RtLeaf> L = &S.leaves[l];
       if (O->leaf_cull) {
         if (L->cull == RT_CULL_ALWAYS) continue;
-        if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, p, dir, inv, tmax)) continue;
+        if (L->cull == RT_CULL_BOX) CNT(cb + 3);
+        if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
       }
+      CNT(cb + 4);
+      CNT(cb + 5 + (L->kind == RT_N_SPHERE ? 0 : L->kind == RT_N_PLANE ? 1 : 2));
       double t0 = 0.0, t1 = 0.0;
-      int n = leaf_candidates(L, p, dir, &t0, &t1);
+      int n = leaf_candidates(L, p, dir, fin, &t0, &t1);
       const bool filtered = L->prog_end != L->prog_begin;
+      if (filtered && ((n >= 1 && t0 > EPS && t0 < dist) || (n >= 2 && t1 > EPS && t1 < dist))) CNT(cb + 8);
       if (n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) {
         tr *= tobj;
         if (tr == 0.0 && S.shadow_early_out) return 0.0;
@@ -359,11 +431,12 @@ __device__ void object_normal_uv(const DS& S, cptr<RtObject> O, V3 p, bool want_
                                  double* u, double* v) {
   cptr<RtNode> N = S.nodes + O->node_begin;
   const int cnt = O->node_count;
+  const bool fin = wave_finite(p);
   *u = 0.0;
   *v = 0.0;
   if (cnt == 1) {
     cptr<RtLeaf> L = &S.leaves[N[0].leaf];
-    *n = leaf_normal(L, p);
+    *n = leaf_normal(L, p, fin);
     if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
     return;
   }
@@ -373,8 +446,8 @@ __device__ void object_normal_uv(const DS& S, cptr<RtObject> O, V3 p, bool want_
     bool bi, bo;
     if (nk < RT_N_UNION) {
       cptr<RtLeaf> L = &S.leaves[nl];
-      bi = leaf_inside(L, p);
-      bo = leaf_on_surface(L, p);
+      bi = leaf_inside(L, p, fin);
+      bo = leaf_on_surface(L, p, fin);
     } else {
       bool ia = (in >> na) & 1u, ib = (in >> nb) & 1u, oa = (on >> na) & 1u, ob = (on >> nb) & 1u;
       if (nk == RT_N_UNION) { bi = ia || ib; bo = (oa && !ib) || (ob && !ia); }
@@ -403,7 +476,7 @@ __device__ void object_normal_uv(const DS& S, cptr<RtObject> O, V3 p, bool want_
   for (int l = lb; l < le; ++l) {
     if (!((__ballot(sel == l) >> lane) & 1)) continue;
     cptr<RtLeaf> L = &S.leaves[l];
-    *n = leaf_normal(L, p);
+    *n = leaf_normal(L, p, fin);
     if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
   }
   if (neg) *n = scale(*n, -1.0);
@@ -441,6 +514,7 @@ __device__ __forceinline__ void shade_inputs(const DS& S, int oi, V3 p, V3* nrm,
                                              double* refl) {
   uint64_t todo = __ballot(oi >= 0);
   while (todo) {
+    CNTW(27);
     const int o = __builtin_amdgcn_readlane(oi, (int)__builtin_ctzll(todo));
     const uint64_t mine = __ballot(oi == o);
     todo &= ~mine;
@@ -519,7 +593,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
     bool descend = false;
     double t_hit;
     PROF_T0(p0);
-    const int oi = nearest_hit(S, ro, rd, &t_hit);
+    const int oi = nearest_hit(S, ro, rd, &t_hit, trip == 0 ? 0 : 1);
     PROF_ADD(trip == 0 ? 0 : 1, p0);
     ++trip;
     PROF_T0(p1);
@@ -661,6 +735,8 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
 __device__ __forceinline__ DS make_ds(const RtDevScene& s) {
   DS d;
   d.objects = as_const(s.objects);
+  d.trav = as_const(s.trav);
+  d.n_trav = s.n_trav;
   d.nodes = as_const(s.nodes);
   d.leaves = as_const(s.leaves);
   d.prog = as_const(s.prog);
@@ -970,13 +1046,14 @@ __global__ __launch_bounds__(256) void ortho_kernel(RtDevScene S, OrthoView V, i
   const V3 ro = {o3[0], o3[1], o3[2]}, rd = {d3[0], d3[1], d3[2]};
   double best = INFINITY;
   int bobj = -1;
+  const bool fin = wave_finite(ro, rd);
   for (int o = 0; o < D.n_objects; ++o) {
     cptr<RtObject> O = &D.objects[o];
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
     for (int l = lb; l < le; ++l) {
       cptr<RtLeaf> L = &D.leaves[l];
       double t0 = 0.0, t1 = 0.0;
-      const int n = leaf_candidates(L, ro, rd, &t0, &t1);
+      const int n = leaf_candidates(L, ro, rd, fin, &t0, &t1);
       const bool filtered = L->prog_end != L->prog_begin;
       if (n >= 1 && t0 < best && (!filtered || leaf_filter(D, L, add(ro, scale(rd, t0))))) { best = t0; bobj = o; }
       if (n >= 2 && t1 < best && (!filtered || leaf_filter(D, L, add(ro, scale(rd, t1))))) { best = t1; bobj = o; }
@@ -1057,6 +1134,16 @@ static size_t put(std::vector<uint8_t>& blob, const std::vector<T>& v) {
 
 extern "C" {
 
+#ifdef RT_COUNT
+__attribute__((visibility("default"))) int rt_diag_cnt(unsigned long long* out32) {
+  if (hipDeviceSynchronize() != hipSuccess) return RT_ERR_DEVICE;
+  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_rt_cnt), 32 * sizeof(unsigned long long)) != hipSuccess) return RT_ERR_DEVICE;
+  static const unsigned long long zero[32] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_rt_cnt), zero, sizeof(zero)) != hipSuccess) return RT_ERR_DEVICE;
+  return RT_OK;
+}
+#endif
+
 #ifdef RT_PROF
 // Diagnostic build only: read-and-reset the section wave-cycle counters (tools/section_profile.py).
 __attribute__((visibility("default"))) int rt_diag_prof(unsigned long long* out8) {
@@ -1100,7 +1187,7 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   int rc = rt::flatten(*s, &f);
   if (rc) return rc;
   std::vector<uint8_t> blob;
-  size_t o_obj = put(blob, f.objects), o_nodes = put(blob, f.nodes), o_leaves = put(blob, f.leaves);
+  size_t o_obj = put(blob, f.objects), o_trav = put(blob, f.trav), o_nodes = put(blob, f.nodes), o_leaves = put(blob, f.leaves);
   size_t o_prog = put(blob, f.prog), o_lights = put(blob, f.lights), o_tex = put(blob, f.textures);
   size_t o_texels = put(blob, f.texels);
   RT_HIP(hipSetDevice(c->device));
@@ -1112,6 +1199,8 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   uint8_t* b = (uint8_t*)c->d_blob;
   RtDevScene& d = c->dev;
   d.objects = (const RtObject*)(b + o_obj);
+  d.trav = (const RtTrav*)(b + o_trav);
+  d.n_trav = (int32_t)f.trav.size();
   d.nodes = (const RtNode*)(b + o_nodes);
   d.leaves = (const RtLeaf*)(b + o_leaves);
   d.prog = (const RtProg*)(b + o_prog);

@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #define RT_EPSILON 10e-7            /* math.rs:2 */
+#define RT_CULL_COORD_MAX 1e6        /* culling boxes / ray origins beyond this are never culled */
 #define RT_MAX_DEPTH_CAP 16          /* recursion frames kept per lane (max_depth <= 16) */
 
 enum RtNodeKind : int32_t {
@@ -68,7 +69,18 @@ struct alignas(16) RtLeaf {
   int32_t prog_begin;   // hit-filter program [prog_begin, prog_end)
   int32_t prog_end;
   int32_t cull;         // RtCull
+  int32_t xdiag;        // inv is diagonal-affine (see below): transform_vector has a 2-op form
+  int32_t pad[3];
 };
+// xdiag: the inverse's 3x3 part is diagonal (off-diagonal entries are +-0) and every entry is
+// finite.  For FINITE inputs transform_vector's row ((m00*x + m01*y) + m02*z) + m03 then equals
+// m00*x + m03 except possibly in the SIGN of an exactly-zero result (the dropped terms are
+// signed zeros: they leave any nonzero partial sum unchanged).  No consumer can observe that
+// sign: object-space points and directions only reach comparisons, fabs, squares and sums with
+// the other components; a zero distance is rejected by `d > EPS` (and compares equal either way
+// in the ortho views); a zero direction component takes the `dir == 0` branch of the cube slab
+// test for both signs.  The kernel takes the short form only when every input of the wave is
+// finite (0 * inf would be NaN in the full form).
 
 struct RtNode {
   int32_t kind;         // RtNodeKind
@@ -91,6 +103,17 @@ struct alignas(16) RtObject {
   int32_t pad2;
 };
 
+// Order-preserving object hierarchy: a pre-order list of nodes over CONTIGUOUS runs of objects
+// in draw order.  A group node's box is the hull of its objects' boxes; a ray that misses it
+// skips to `skip`.  Objects are still visited in increasing index order, so the nearest-hit tie
+// rule (first object wins) and the shadow product order are the reference's.
+struct alignas(16) RtTrav {
+  double blo[3], bhi[3];
+  int32_t obj;                      // >= 0: object index; -1: group node
+  int32_t skip;                     // node index after this node's subtree
+  int32_t pad[2];
+};
+
 struct RtTexture {
   int64_t offset;                   // byte offset of RGBA8 data in the texel pool
   int32_t w, h;
@@ -106,13 +129,14 @@ struct RtCamera {
 // Kernel argument block (passed by value; all pointers are device pointers).
 struct RtDevScene {
   const RtObject* objects;
+  const RtTrav* trav;
   const RtNode* nodes;
   const RtLeaf* leaves;
   const RtProg* prog;
   const RtLight* lights;
   const RtTexture* textures;
   const uint8_t* texels;
-  int32_t n_objects, n_lights, n_leaves, n_nodes;
+  int32_t n_objects, n_lights, n_leaves, n_nodes, n_trav, pad0;
   int32_t width, height;
   int32_t any_transparent;          // some object has transparency != 0 (refraction possible)
   int32_t shadow_early_out;         // every transparency is finite: product==0 stays 0

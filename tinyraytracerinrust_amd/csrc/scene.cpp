@@ -8,6 +8,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <cmath>
 #include <new>
 #include <string>
 #include <vector>
@@ -125,6 +126,16 @@ static void leaf_common(const rt_transformation& t, RtLeaf* L) {
   V mo = apply(t.matrix, {0.0, 0.0, 0.0});
   L->inv_o[0] = io.x; L->inv_o[1] = io.y; L->inv_o[2] = io.z;
   L->mat_o[0] = mo.x; L->mat_o[1] = mo.y; L->mat_o[2] = mo.z;
+  // diagonal-affine inverse (rt_blob.h): off-diagonals +-0, all entries finite
+  const double* m = t.inverse;
+  bool diag = true;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 4; ++j) {
+      const double v = m[4 * i + j];
+      if (!std::isfinite(v)) diag = false;
+      if (j < 3 && j != i && v != 0.0) diag = false;
+    }
+  L->xdiag = diag ? 1 : 0;
 }
 
 // MathPlane::new (math_shapes.rs:140-152): raw (a,b,c,d) + transformed unit normal.
@@ -250,7 +261,9 @@ static Box leaf_box(const ShapeRec& s) {
     long double margin = 1e-6L * (fabsl(wc) + half[i]) + 1e-6L;
     r.lo[i] = (double)(wc - half[i] - margin);
     r.hi[i] = (double)(wc + half[i] + margin);
-    if (!isfinite(r.lo[i]) || !isfinite(r.hi[i])) return box_infinite();
+    // the kernel's slab arithmetic is only proven conservative for coordinates within 1e6
+    // (render_kernels.hip cull_ray): larger boxes are never culled
+    if (!(fabs(r.lo[i]) <= RT_CULL_COORD_MAX) || !(fabs(r.hi[i]) <= RT_CULL_COORD_MAX)) return box_infinite();
   }
   return r;
 }
@@ -311,6 +324,74 @@ struct Flattener {
   }
 };
 
+// ---------------------------------------------------------------- object hierarchy
+static double box_area(const double* lo, const double* hi) {
+  const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+  return 2.0 * (x * y + y * z + z * x);
+}
+
+struct HierBuilder {
+  FlatScene& f;
+  void hull(int a, int b, double* lo, double* hi) const {
+    for (int k = 0; k < 3; ++k) { lo[k] = INFINITY; hi[k] = -INFINITY; }
+    for (int o = a; o < b; ++o)
+      for (int k = 0; k < 3; ++k) {
+        lo[k] = fmin(lo[k], f.objects[o].blo[k]);
+        hi[k] = fmax(hi[k], f.objects[o].bhi[k]);
+      }
+  }
+  void object(int o) {
+    RtTrav t;
+    memset(&t, 0, sizeof t);
+    t.obj = o;
+    t.skip = (int32_t)f.trav.size() + 1;
+    f.trav.push_back(t);
+  }
+  // Objects [a, b), all with a finite box.  A group node is emitted when it is clearly smaller
+  // than the enclosing group (surface area); the run is split where the SAH cost is lowest.
+  void run(int a, int b, double parent_area) {
+    if (b - a == 1) { object(a); return; }
+    RtTrav g;
+    memset(&g, 0, sizeof g);
+    hull(a, b, g.blo, g.bhi);
+    const double area = box_area(g.blo, g.bhi);
+    const bool group = area <= 0.8 * parent_area;
+    const size_t gi = f.trav.size();
+    if (group) { g.obj = -1; f.trav.push_back(g); parent_area = area; }
+    if (b - a == 2) {
+      object(a);
+      object(a + 1);
+    } else {
+      int best_k = a + 1;
+      double best = INFINITY;
+      for (int k = a + 1; k < b; ++k) {
+        double lo[3], hi[3], lo2[3], hi2[3];
+        hull(a, k, lo, hi);
+        hull(k, b, lo2, hi2);
+        const double cost = box_area(lo, hi) * (k - a) + box_area(lo2, hi2) * (b - k);
+        if (cost < best) { best = cost; best_k = k; }
+      }
+      run(a, best_k, parent_area);
+      run(best_k, b, parent_area);
+    }
+    if (group) f.trav[gi].skip = (int32_t)f.trav.size();
+  }
+};
+
+static void build_hierarchy(FlatScene* fs) {
+  HierBuilder h{*fs};
+  fs->trav.clear();
+  const int n = (int)fs->objects.size();
+  const bool flat = getenv("RT_FLAT_OBJECTS") != nullptr;   // diagnostic: no group nodes
+  for (int i = 0; i < n;) {
+    if (flat || fs->objects[i].cull != RT_CULL_BOX) { h.object(i); ++i; continue; }
+    int j = i;
+    while (j < n && fs->objects[j].cull == RT_CULL_BOX) ++j;
+    h.run(i, j, INFINITY);
+    i = j;
+  }
+}
+
 int flatten(const rt_scene& s, FlatScene* out) {
   FlatScene& f = *out;
   f = FlatScene();
@@ -358,11 +439,17 @@ int flatten(const rt_scene& s, FlatScene* out) {
       L.cull = useful.kind;
       for (int i = 0; i < 3; ++i) { L.blo[i] = useful.lo[i]; L.bhi[i] = useful.hi[i]; }
       obox = box_hull(obox, useful);
-      if (useful.kind != RT_CULL_NONE) ++n_leaf_boxes_tighter;
     }
     ob.cull = obox.kind;
     for (int i = 0; i < 3; ++i) { ob.blo[i] = obox.lo[i]; ob.bhi[i] = obox.hi[i]; }
-    ob.leaf_cull = ob.leaf_count > 1 && n_leaf_boxes_tighter > 0;
+    // per-leaf box tests only pay when some leaf box is clearly tighter than the object's
+    for (int32_t l = ob.leaf_begin; l < ob.leaf_begin + ob.leaf_count && ob.leaf_count > 1; ++l) {
+      const RtLeaf& L = f.leaves[l];
+      if (L.cull == RT_CULL_ALWAYS) ++n_leaf_boxes_tighter;
+      else if (L.cull == RT_CULL_BOX && (ob.cull == RT_CULL_NONE || box_area(L.blo, L.bhi) < 0.8 * box_area(ob.blo, ob.bhi)))
+        ++n_leaf_boxes_tighter;
+    }
+    ob.leaf_cull = n_leaf_boxes_tighter > 0;
     const rt_material& m = o.mat;
     ob.textured = m.texture >= 0;
     ob.tex = m.texture >= 0 ? m.texture : 0;
@@ -375,6 +462,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
     if (!isfinite(m.transparency)) f.shadow_early_out = 0;
     f.objects.push_back(ob);
   }
+  build_hierarchy(&f);
   for (const LightRec& l : s.lights) {
     RtLight L;
     for (int i = 0; i < 3; ++i) { L.p[i] = l.p[i]; L.col[i] = l.color[i]; }
@@ -390,14 +478,17 @@ int flatten(const rt_scene& s, FlatScene* out) {
     while (off % 16) { f.texels.push_back(0); ++off; }
   }
   if (getenv("RT_DUMP_FLAT")) {                                // debugging aid: culling boxes
+    for (size_t i = 0; i < f.trav.size(); ++i)
+      fprintf(stderr, "trav %zu obj=%d skip=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f]\n", i, f.trav[i].obj, f.trav[i].skip,
+              f.trav[i].blo[0], f.trav[i].blo[1], f.trav[i].blo[2], f.trav[i].bhi[0], f.trav[i].bhi[1], f.trav[i].bhi[2]);
     for (size_t o = 0; o < f.objects.size(); ++o) {
       const RtObject& ob = f.objects[o];
       fprintf(stderr, "object %zu cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] leaves %d leaf_cull=%d\n", o, ob.cull,
               ob.blo[0], ob.blo[1], ob.blo[2], ob.bhi[0], ob.bhi[1], ob.bhi[2], ob.leaf_count, ob.leaf_cull);
       for (int l = ob.leaf_begin; l < ob.leaf_begin + ob.leaf_count; ++l) {
         const RtLeaf& L = f.leaves[l];
-        fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d\n", l, L.kind, L.cull,
-                L.blo[0], L.blo[1], L.blo[2], L.bhi[0], L.bhi[1], L.bhi[2], L.prog_end - L.prog_begin);
+        fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d xdiag %d\n", l, L.kind, L.cull,
+                L.blo[0], L.blo[1], L.blo[2], L.bhi[0], L.bhi[1], L.bhi[2], L.prog_end - L.prog_begin, L.xdiag);
       }
     }
   }
@@ -463,6 +554,16 @@ int rt_scene_new(uint32_t width, uint32_t height, rt_scene** out) {
   s->width = width;
   s->height = height;
   *out = s;
+  return RT_OK;
+}
+
+int rt_scene_traversal(const rt_scene* s, int32_t* obj, int32_t* skip, int32_t cap, int32_t* n) {
+  if (!s || !n || cap < 0 || (cap > 0 && (!obj || !skip))) return fail(RT_ERR_INVALID, "null argument");
+  FlatScene f;
+  int rc = flatten(*s, &f);
+  if (rc) return rc;
+  *n = (int32_t)f.trav.size();
+  for (int32_t i = 0; i < *n && i < cap; ++i) { obj[i] = f.trav[i].obj; skip[i] = f.trav[i].skip; }
   return RT_OK;
 }
 

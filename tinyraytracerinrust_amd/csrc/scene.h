@@ -40,6 +40,7 @@ struct TextureRec { uint32_t w, h; std::vector<uint8_t> rgba; };
 // Flattened scene, host copy of what goes to HBM.
 struct FlatScene {
   std::vector<RtObject> objects;
+  std::vector<RtTrav> trav;
   std::vector<RtNode> nodes;
   std::vector<RtLeaf> leaves;
   std::vector<RtProg> prog;

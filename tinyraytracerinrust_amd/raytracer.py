@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Iterable, Iterator, Optional, Sequence, Tuple
+from typing import Iterable, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -141,6 +141,14 @@ class Scene:
                                   ctypes.byref(w), ctypes.byref(h)))
         return {"objects": no.value, "lights": nl.value, "leaves": nlf.value,
                 "width": w.value, "height": h.value}
+
+    def traversal(self) -> List[Tuple[int, int]]:
+        """The kernels' object hierarchy: pre-order (obj, skip) nodes, obj = -1 for a group."""
+        n = ctypes.c_int32()
+        check(lib().rt_scene_traversal(self.h, None, None, 0, ctypes.byref(n)))
+        obj, skip = (ctypes.c_int32 * max(1, n.value))(), (ctypes.c_int32 * max(1, n.value))()
+        check(lib().rt_scene_traversal(self.h, obj, skip, n.value, ctypes.byref(n)))
+        return [(obj[i], skip[i]) for i in range(n.value)]
 
     def camera(self) -> dict:
         out = (ctypes.c_double * 13)()
