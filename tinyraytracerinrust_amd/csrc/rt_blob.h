@@ -22,6 +22,7 @@
 #define RT_EPSILON 10e-7            /* math.rs:2 */
 #define RT_CULL_COORD_MAX 1e6        /* culling boxes / ray origins beyond this are never culled */
 #define RT_MAX_DEPTH_CAP 16          /* recursion frames kept per lane (max_depth <= 16) */
+#define RT_MAX_LITS 4                /* inline hit-filter literals per leaf */
 
 enum RtNodeKind : int32_t {
   RT_N_SPHERE = 0, RT_N_PLANE = 1, RT_N_CUBE = 2,
@@ -70,8 +71,14 @@ struct alignas(16) RtLeaf {
   int32_t prog_end;
   int32_t cull;         // RtCull
   int32_t xdiag;        // inv is diagonal-affine (see below): transform_vector has a 2-op form
-  int32_t pad[3];
+  int32_t n_lit;        // >= 0: the filter program is the conjunction of n_lit literals below
+  int32_t lit[RT_MAX_LITS];   // literal = 2 * leaf + want: leaf[lit >> 1].is_inside(p) == (lit & 1)
+  int32_t pad[2];
 };
+// Literal form: most CSG filters (every ancestor requiring an intersection / difference sibling
+// inside, or a union sibling outside) are a plain conjunction of single-leaf is_inside tests;
+// the host rewrites the postfix program into at most RT_MAX_LITS literals (n_lit = -1: keep the
+// program).  The tests are pure, so their order is free.
 // xdiag: the inverse's 3x3 part is diagonal (off-diagonal entries are +-0) and every entry is
 // finite.  For FINITE inputs transform_vector's row ((m00*x + m01*y) + m02*z) + m03 then equals
 // m00*x + m03 except possibly in the SIGN of an exactly-zero result (the dropped terms are

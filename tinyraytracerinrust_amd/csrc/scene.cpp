@@ -8,7 +8,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cmath>
+#include <functional>
 #include <new>
 #include <string>
 #include <vector>
@@ -324,6 +326,51 @@ struct Flattener {
   }
 };
 
+// ---------------------------------------------------------------- hit-filter literal form
+// Rewrite a leaf's postfix filter program [b, e) into a conjunction of literals (2*leaf + want)
+// when every REQUIRE reduces to one: v == 1 of AND / ANDNOT and v == 0 of OR distribute over
+// their operands; anything else (a disjunction) keeps the program.  Returns the literal count,
+// or -1.
+static int filter_literals(const std::vector<RtProg>& prog, int32_t b, int32_t e, int32_t* lits) {
+  struct Fm { int32_t op, leaf, a, b; };
+  std::vector<Fm> fm;
+  std::vector<int32_t> st;
+  std::vector<int32_t> out;
+  bool ok = true;
+  std::function<void(int32_t, int32_t)> conj = [&](int32_t x, int32_t want) {
+    const Fm& f = fm[x];
+    if (f.op == RT_OP_INSIDE) { out.push_back(2 * f.leaf + want); return; }
+    if (want == 1 && f.op == RT_OP_AND) { conj(f.a, 1); conj(f.b, 1); return; }
+    if (want == 1 && f.op == RT_OP_ANDNOT) { conj(f.a, 1); conj(f.b, 0); return; }
+    if (want == 0 && f.op == RT_OP_OR) { conj(f.a, 0); conj(f.b, 0); return; }
+    ok = false;
+  };
+  for (int32_t k = b; k < e && ok; ++k) {
+    const RtProg& p = prog[k];
+    if (p.op == RT_OP_INSIDE) {
+      fm.push_back({RT_OP_INSIDE, p.arg, -1, -1});
+      st.push_back((int32_t)fm.size() - 1);
+    } else if (p.op == RT_OP_REQUIRE) {
+      if (st.empty()) return -1;
+      conj(st.back(), p.arg);
+      st.pop_back();
+    } else {
+      if (st.size() < 2) return -1;
+      const int32_t y = st.back(); st.pop_back();
+      const int32_t x = st.back(); st.pop_back();
+      fm.push_back({p.op, -1, x, y});
+      st.push_back((int32_t)fm.size() - 1);
+    }
+  }
+  if (!ok || !st.empty()) return -1;
+  std::vector<int32_t> uniq;
+  for (int32_t v : out)
+    if (std::find(uniq.begin(), uniq.end(), v) == uniq.end()) uniq.push_back(v);
+  if (uniq.size() > RT_MAX_LITS) return -1;
+  for (size_t i = 0; i < uniq.size(); ++i) lits[i] = uniq[i];
+  return (int32_t)uniq.size();
+}
+
 // ---------------------------------------------------------------- object hierarchy
 static double box_area(const double* lo, const double* hi) {
   const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
@@ -436,6 +483,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
       }
       RtLeaf& L = f.leaves[n.leaf];
       L.prog_end = (int32_t)f.prog.size();
+      L.n_lit = filter_literals(f.prog, L.prog_begin, L.prog_end, L.lit);
       L.cull = useful.kind;
       for (int i = 0; i < 3; ++i) { L.blo[i] = useful.lo[i]; L.bhi[i] = useful.hi[i]; }
       obox = box_hull(obox, useful);
@@ -487,8 +535,8 @@ int flatten(const rt_scene& s, FlatScene* out) {
               ob.blo[0], ob.blo[1], ob.blo[2], ob.bhi[0], ob.bhi[1], ob.bhi[2], ob.leaf_count, ob.leaf_cull);
       for (int l = ob.leaf_begin; l < ob.leaf_begin + ob.leaf_count; ++l) {
         const RtLeaf& L = f.leaves[l];
-        fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d xdiag %d\n", l, L.kind, L.cull,
-                L.blo[0], L.blo[1], L.blo[2], L.bhi[0], L.bhi[1], L.bhi[2], L.prog_end - L.prog_begin, L.xdiag);
+        fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d lits %d xdiag %d\n", l, L.kind, L.cull,
+                L.blo[0], L.blo[1], L.blo[2], L.bhi[0], L.bhi[1], L.bhi[2], L.prog_end - L.prog_begin, L.n_lit, L.xdiag);
       }
     }
   }

@@ -1,0 +1,60 @@
+"""Interleaved A/B kernel timing of several builds of librt_mi355x.so in ONE process (diagnostic).
+
+Each library is loaded with its own ctypes handle (RTLD_LOCAL, so identical symbol names do not
+clash), gets its own context and scene upload, and the 4K globes frame is rendered round-robin
+over the libraries REPS times; the median / min kernel ms per library are printed.  Interleaving
+cancels clock drift (DVFS) between variants, which separate runs do not.
+usage: python tools/ab_interleaved.py LIB [LIB ...] [--reps N] [--depth D] [--size WxH] [--scene NAME]
+"""
+import argparse
+import ctypes
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCENES = os.path.join(ROOT, "tests", "golden", "scenes")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--depth", type=int, default=10)
+    ap.add_argument("--size", default="3840x2160")
+    ap.add_argument("--scene", default="globes")
+    ap.add_argument("--time", type=float, default=0.0)
+    a = ap.parse_args()
+    import torch
+    W, H = (int(v) for v in a.size.split("x"))
+    text = open(os.path.join(SCENES, a.scene + ".scene")).read().encode()
+    out = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    ctxs = []
+    for path in a.libs:
+        L = ctypes.CDLL(os.path.abspath(path))
+        sc, cx = ctypes.c_void_p(), ctypes.c_void_p()
+        assert L.rt_scene_compile(text, SCENES.encode(), ctypes.c_double(a.time), W, H, ctypes.byref(sc)) == 0
+        assert L.rt_ctx_create(0, ctypes.byref(cx)) == 0
+        assert L.rt_ctx_upload(cx, sc) == 0
+        ctxs.append((path, L, cx, []))
+    for rep in range(a.reps + 3):
+        for path, L, cx, ms in ctxs:
+            rc = L.rt_render_rows(cx, 0, H, a.depth, ctypes.c_void_p(out.data_ptr()), ctypes.c_size_t(W * 4),
+                                  ctypes.c_void_p(st))
+            assert rc == 0, rc
+            torch.cuda.synchronize()
+            v = ctypes.c_float()
+            L.rt_ctx_last_kernel_ms(cx, ctypes.byref(v))
+            if rep >= 3:
+                ms.append(v.value)
+    base = None
+    for path, L, cx, ms in ctxs:
+        med = statistics.median(ms)
+        base = base or med
+        print(f"{a.scene} {W}x{H} d={a.depth}  median {med:.4f} ms  min {min(ms):.4f}  ({med / base:.3f}x of first)  {path}",
+              flush=True)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -23,10 +23,14 @@ def main():
     ap.add_argument("--time", type=float, default=0.0)
     ap.add_argument("--depth", type=int, default=10)
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--frames", type=int, default=0,
+                    help="animation mode: per-frame totals of frames f = 0..F-1 at time f/F (BASELINE config 5)")
     a = ap.parse_args()
     scenes = os.path.join(ROOT, "tests", "golden", "scenes")
     O.register_texture_file("worldmap.png", os.path.join(scenes, "worldmap.png"))
     text = open(os.path.join(scenes, a.scene + ".scene")).read()
+    if a.frames:
+        return animation(a, text)
     sc = O.OracleScene(text, a.time, a.width, a.height, max_depth=a.depth, counting=True)
     rows, totals = [], {}
     for y in range(a.height):
@@ -44,6 +48,27 @@ def main():
     with open(path, "w") as f:
         json.dump(out, f)
     print(path, totals["flop"], "flops,", totals["flop"] / (a.width * a.height), "per pixel")
+
+
+def animation(a, text):
+    """Per-frame totals of an F-frame animation (time = f / F), whole frames."""
+    frames, totals = [], {}
+    for f in range(a.frames):
+        sc = O.OracleScene(text, f / a.frames, a.width, a.height, max_depth=a.depth, counting=True)
+        _, _, c = sc.render(0, a.height, threads=a.threads, u8=False)
+        frames.append(c["flop"])
+        for k, v in c.items():
+            totals[k] = totals.get(k, 0) + v
+        print(f"frame {f}: {c['flop']} flops", flush=True)
+    out = {
+        "scene": a.scene + ".scene", "width": a.width, "height": a.height, "frames": a.frames,
+        "time": "f / frames", "max_depth": a.depth, "flop_definition": "as flops_globes_*.json",
+        "totals": totals, "frame_flops": frames,
+    }
+    path = os.path.join(ROOT, "tests", "golden", f"flops_{a.scene}_{a.width}x{a.height}_anim{a.frames}_d{a.depth}.json")
+    with open(path, "w") as f:
+        json.dump(out, f)
+    print(path, totals["flop"], "flops")
 
 
 if __name__ == "__main__":
