@@ -157,6 +157,16 @@ int rt_render_rows(rt_ctx* ctx, uint32_t y0, uint32_t y1, int32_t max_depth,
 int rt_render_row_bands(rt_ctx* ctx, uint32_t y_first, uint32_t band_rows, uint32_t band_pitch,
                         uint32_t n_bands, int32_t max_depth, uint8_t* rgba8, size_t row_stride_bytes,
                         void* stream);
+/* Frame assembly after the multi-GPU all-gather (the GTK thread's apply_line placing every
+ * worker's rows at their y, debug_window.rs:147-163, for all ranks at once).  `gathered` holds
+ * `world` slots of slot_rows rows in rank order, each rank's rt_render_row_bands output for the
+ * band layout above: frame row y is in band b = y / band_rows, which rank b % world packed at its
+ * slot row (b / world) * band_rows + y % band_rows (a contiguous tile per rank: band_rows =
+ * slot_rows).  Writes frame rows [0, height) of row_bytes bytes.  Device pointers only, one launch
+ * on `stream`, asynchronous. */
+int rt_assemble_row_bands(const uint8_t* gathered, size_t gathered_stride, uint32_t world, uint32_t slot_rows,
+                          uint32_t band_rows, uint32_t height, size_t row_bytes, uint8_t* frame,
+                          size_t frame_stride, void* stream);
 /* Same as rt_render_rows, pre-quantisation colours: 4 doubles per pixel (r,g,b,a) -- the
  * `Vec<Color>` rows. */
 int rt_render_rows_f64(rt_ctx* ctx, uint32_t y0, uint32_t y1, int32_t max_depth,

@@ -201,6 +201,29 @@ def test_row_bands_assemble_like_ranks(T, world, layout, band):
     for rank in range(world):
         y_first, band_rows, pitch, n_bands = D.band_params(H, world, rank, layout, band)
         r.render_row_bands(y_first, band_rows, pitch, n_bands, gath[rank * slot_rows:(rank + 1) * slot_rows])
-    frame = D.assemble(gath, H, world, layout, band)
+    frame = D.assemble(gath, H, world, layout, band)                     # rt_assemble_row_bands
+    ref = D.assemble_reference(gath, H, world, layout, band)             # torch restatement
+    into = D.assemble(gath, H, world, layout, band, out=torch.empty_like(ref))
     torch.cuda.synchronize()
     assert np.array_equal(frame.cpu().numpy(), full)
+    assert np.array_equal(ref.cpu().numpy(), full)
+    assert np.array_equal(into.cpu().numpy(), full)
+
+
+@pytest.mark.parametrize("W,world,band", [(3840, 8, 8), (33, 3, 5), (7, 2, 1)])
+def test_assemble_row_bands_kernel(T, W, world, band):
+    """rt_assemble_row_bands on random bytes against the torch permutation, including row lengths
+    that are not a multiple of 16 bytes (byte-copy path) and strided (padded) rows."""
+    import torch
+    from tinyraytracerinrust_amd import distributed as D
+    H = 2160 if W == 3840 else 61
+    slot_rows = D.rows_per_rank(H, world, "cyclic", band)
+    g = torch.randint(0, 256, (world * slot_rows, W, 4), dtype=torch.uint8, device="cuda")
+    want = D.assemble_reference(g, H, world, "cyclic", band).cpu()
+    got = D.assemble(g, H, world, "cyclic", band).cpu()
+    assert torch.equal(got, want)
+    padded = torch.zeros((H, W + 3, 4), dtype=torch.uint8, device="cuda")[:, :W]   # row stride > row bytes
+    D._assemble_device(g, H, world, slot_rows, band, out=padded)
+    assert torch.equal(padded.cpu(), want)
+    with pytest.raises(T.RtError):                                      # slot too small for the layout
+        D._assemble_device(g[: world * (slot_rows - band)], H, world, slot_rows - band, band)

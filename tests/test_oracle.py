@@ -123,6 +123,11 @@ def test_flop_fixture_consistent():
     for name in os.listdir(GOLDEN):
         if name.startswith("flops_") and name.endswith(".json"):
             d = json.load(open(os.path.join(GOLDEN, name)))
+            if "frame_flops" in d:                               # animation: one entry per frame
+                assert sum(d["frame_flops"]) == d["totals"]["flop"]
+                assert len(d["frame_flops"]) == d["frames"]
+                assert d["totals"]["ray_primary"] == d["width"] * d["height"] * d["frames"]
+                continue
             assert sum(d["row_flops"]) == d["totals"]["flop"]
             assert len(d["row_flops"]) == d["height"]
             assert d["totals"]["ray_primary"] == d["width"] * d["height"]

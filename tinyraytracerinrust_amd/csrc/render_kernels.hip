@@ -582,12 +582,40 @@ struct BufRec {
   }
 };
 
+// Frame-stack slots in LDS.  The first KL frames of every lane's stack (A.r, A.g, A.b, w) live in
+// LDS laid out [frame][component][lane], so each access is one conflict-free ds_*_b64; deeper
+// frames (chains longer than KL, rare) use the private array, i.e. scratch.  8 KB per wave for
+// KL = 4: 16 one-wave workgroups per CU (4 waves/SIMD) take 128 of the 160 KB.  Measured on
+// MI355X (profiles/r01r_lds_stack_ab.txt): KL = 4 is 0.2-0.8 % SLOWER than the scratch stack at
+// 4K globes d=10 (the pushes are fire-and-forget and the pops few), so the product keeps KL = 0;
+// -DRT_LDS_FRAMES=4 builds the variant.
+#define LDS_AS __attribute__((address_space(3)))
+typedef LDS_AS double lds_f64;
+#ifndef RT_LDS_FRAMES
+#define RT_LDS_FRAMES 0
+#endif
+
 // get_ray_color (raytracer.rs:132-287) for one primary ray, recursion unrolled onto a per-lane
 // frame stack.  REFR = the scene has a transparent object (refraction frames need more state).
-template <bool REFR, class Rec = NoRec>
-__device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr) {
+// KL > 0: frames 0..KL-1 of the stack are in LDS at lf[(f * 4 + c) * 64] (lf = this lane's slot).
+template <bool REFR, class Rec = NoRec, int KL = 0>
+__device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, lds_f64* lf = nullptr) {
   double fA[RT_MAX_DEPTH_CAP][3];     // parent colour already intensified by (1 - w)
   double fW[RT_MAX_DEPTH_CAP];        // child weight w (transparency or reflectivity)
+  auto put_frame = [&](int f, Col A, double w) {
+    if (KL > 0 && f < KL) {
+      lf[(f * 4 + 0) * 64] = A.r; lf[(f * 4 + 1) * 64] = A.g; lf[(f * 4 + 2) * 64] = A.b; lf[(f * 4 + 3) * 64] = w;
+    } else {
+      fA[f][0] = A.r; fA[f][1] = A.g; fA[f][2] = A.b; fW[f] = w;
+    }
+  };
+  auto get_frame = [&](int f, Col* A, double* w) {
+    if (KL > 0 && f < KL) {
+      *A = {lf[(f * 4 + 0) * 64], lf[(f * 4 + 1) * 64], lf[(f * 4 + 2) * 64]}; *w = lf[(f * 4 + 3) * 64];
+    } else {
+      *A = {fA[f][0], fA[f][1], fA[f][2]}; *w = fW[f];
+    }
+  };
   double fP[REFR ? RT_MAX_DEPTH_CAP : 1][3], fD[REFR ? RT_MAX_DEPTH_CAP : 1][3];
   double fRP[REFR ? RT_MAX_DEPTH_CAP : 1];
   int fPend[REFR ? RT_MAX_DEPTH_CAP : 1];
@@ -679,9 +707,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
       const double rp = tir ? refl + (1.0 - refl) * transp : refl;       // :261-265
       const bool do_refl = depth < max_depth && rp != 0.0 && (!inside || tir);   // :267
       if (do_refr && !tir) {
-        Col A = intensify(L, 1.0 - transp);
-        fA[sp][0] = A.r; fA[sp][1] = A.g; fA[sp][2] = A.b;
-        fW[sp] = transp;
+        put_frame(sp, intensify(L, 1.0 - transp), transp);
         if constexpr (REFR) {
           fPend[sp] = do_refl ? 1 : 0;
           if (do_refl) {
@@ -698,9 +724,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
         depth = sp;
         descend = true;
       } else if (do_refl) {
-        Col A = intensify(L, 1.0 - rp);
-        fA[sp][0] = A.r; fA[sp][1] = A.g; fA[sp][2] = A.b;
-        fW[sp] = rp;
+        put_frame(sp, intensify(L, 1.0 - rp), rp);
         if constexpr (REFR) fPend[sp] = 0;
         if constexpr (RECORD) { fSlot[sp] = slot; ray_type = 1; }        // ReflectionRay
         ++sp;
@@ -717,13 +741,14 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
     if (descend) continue;
     while (sp > 0) {                                                      // post-order combine
       const int f = sp - 1;
-      const Col comb = cadd(Col{fA[f][0], fA[f][1], fA[f][2]}, intensify(C, fW[f]));
+      Col fa;
+      double fw;
+      get_frame(f, &fa, &fw);
+      const Col comb = cadd(fa, intensify(C, fw));
       if constexpr (REFR) {
         if (fPend[f]) {                                                   // refraction done -> reflection
           fPend[f] = 0;
-          Col A = intensify(comb, 1.0 - fRP[f]);
-          fA[f][0] = A.r; fA[f][1] = A.g; fA[f][2] = A.b;
-          fW[f] = fRP[f];
+          put_frame(f, intensify(comb, 1.0 - fRP[f]), fRP[f]);
           ro = {fP[f][0], fP[f][1], fP[f][2]};
           rd = {fD[f][0], fD[f][1], fD[f][2]};
           depth = sp;
@@ -800,7 +825,13 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   V3 ro, rd;
   PROF_T0(p5);
   camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
+#if RT_LDS_FRAMES > 0
+  __shared__ double s_frames[RT_WG_WX * RT_WG_WY][RT_LDS_FRAMES * 4 * 64];   // frame stack, see trace()
+  lds_f64* lf = (lds_f64*)&s_frames[wave][lane];
+  const Col c = trace<REFR, NoRec, RT_LDS_FRAMES>(make_ds(S), ro, rd, max_depth, nullptr, lf);
+#else
   const Col c = trace<REFR>(make_ds(S), ro, rd, max_depth);
+#endif
   PROF_ADD(5, p5);
   uint8_t* row = out + (size_t)r * stride;
   if constexpr (F64) {
@@ -1097,6 +1128,25 @@ __global__ __launch_bounds__(256) void ortho_kernel(RtDevScene S, OrthoView V, i
   }
 }
 
+// ====================================================================== multi-GPU frame assembly
+// Row-band layout (distributed.py): frame row y is in band b = y / band_rows, dealt to rank
+// b % world, which packed it at slot row (b / world) * band_rows + y % band_rows.  After the
+// all-gather (slots in rank order) one launch puts every row at its y -- the GTK thread's
+// apply_line (debug_window.rs:147-163) for all ranks at once.  A contiguous tile per rank is the
+// case band_rows = slot_rows.  One workgroup per row, 16-byte copies when every address allows.
+__global__ __launch_bounds__(256) void assemble_bands_kernel(const uint8_t* __restrict__ g, size_t gstride, int world,
+                                                             int slot_rows, int band, size_t row_bytes,
+                                                             uint8_t* __restrict__ f, size_t fstride, int vec16) {
+  const int y = blockIdx.x, b = y / band;
+  const uint8_t* s = g + ((size_t)(b % world) * slot_rows + (size_t)(b / world) * band + y % band) * gstride;
+  uint8_t* d = f + (size_t)y * fstride;
+  if (vec16) {
+    for (size_t i = threadIdx.x; i < row_bytes / 16; i += blockDim.x) ((uint4*)d)[i] = ((const uint4*)s)[i];
+  } else {
+    for (size_t i = threadIdx.x; i < row_bytes; i += blockDim.x) d[i] = s[i];
+  }
+}
+
 }  // namespace
 
 // ====================================================================== device context
@@ -1305,6 +1355,27 @@ int rt_render_rows(rt_ctx* c, uint32_t y0, uint32_t y1, int32_t max_depth, uint8
 int rt_render_rows_f64(rt_ctx* c, uint32_t y0, uint32_t y1, int32_t max_depth, double* rgba,
                        size_t row_stride_bytes, void* stream) {
   return launch_rows(c, y0, y1, max_depth, rgba, row_stride_bytes, stream, true);
+}
+
+int rt_assemble_row_bands(const uint8_t* gathered, size_t gathered_stride, uint32_t world, uint32_t slot_rows,
+                          uint32_t band_rows, uint32_t height, size_t row_bytes, uint8_t* frame, size_t frame_stride,
+                          void* stream) {
+  if (!gathered || !frame) return fail(RT_ERR_INVALID, "null argument");
+  if (world == 0 || band_rows == 0) return fail(RT_ERR_INVALID, "world and band_rows must be > 0");
+  if (height == 0 || row_bytes == 0) return RT_OK;
+  if (height > (1u << 24)) return fail(RT_ERR_INVALID, "too many rows");
+  const uint64_t bands = ((uint64_t)height + band_rows - 1) / band_rows, per_rank = (bands + world - 1) / world;
+  if ((uint64_t)slot_rows < per_rank * band_rows)
+    return fail(RT_ERR_INVALID, "slot of %u rows holds fewer than %llu bands of %u rows", slot_rows,
+                (unsigned long long)per_rank, band_rows);
+  if (slot_rows > (1u << 24) || (uint64_t)slot_rows * world > (1u << 30)) return fail(RT_ERR_INVALID, "slot too large");
+  if (gathered_stride < row_bytes || frame_stride < row_bytes) return fail(RT_ERR_INVALID, "row stride < row bytes");
+  if (!is_device_ptr(gathered) || !is_device_ptr(frame)) return fail(RT_ERR_INVALID, "frame assembly takes device pointers");
+  const bool v16 = (((uintptr_t)gathered | (uintptr_t)frame | gathered_stride | frame_stride | row_bytes) & 15) == 0;
+  hipLaunchKernelGGL(assemble_bands_kernel, dim3(height), dim3(256), 0, (hipStream_t)stream, gathered, gathered_stride,
+                     (int)world, (int)slot_rows, (int)band_rows, row_bytes, frame, frame_stride, v16 ? 1 : 0);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
 }
 
 // antialiaser.rs:87-191 over a whole quantised frame (see the kernels above).

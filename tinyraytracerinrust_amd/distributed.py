@@ -72,9 +72,43 @@ def assemble(gathered: torch.Tensor, height: int, world: int, layout: str, band:
              out: torch.Tensor = None) -> torch.Tensor:
     """gathered: (world * slot_rows, W, 4) in rank order -> (H, W, 4) frame.
 
-    Contiguous tiles are already in frame order (a view).  Cyclic slots hold bands
-    g = b * world + rank at slot rows [b * band, (b + 1) * band), so the frame is ONE permuted
-    copy: view (world, bands_per_rank, band, ...) -> swap the first two axes -> first H rows."""
+    On a GPU tensor this is ONE launch of the library's row-placement kernel
+    (rt_assemble_row_bands, 16-byte row copies); on CPU tensors (gloo) the torch restatement
+    assemble_reference below, which the GPU tests compare it with."""
+    if not gathered.is_cuda:
+        return assemble_reference(gathered, height, world, layout, band, out)
+    slot_rows = gathered.shape[0] // world
+    if layout == "contiguous" and out is None:
+        return gathered[:height]                                  # already in frame order: a view
+    band_rows = slot_rows if layout == "contiguous" else band
+    return _assemble_device(gathered, height, world, slot_rows, band_rows, out)
+
+
+def _assemble_device(gathered: torch.Tensor, height: int, world: int, slot_rows: int, band_rows: int,
+                     out: torch.Tensor = None) -> torch.Tensor:
+    import ctypes
+    from . import _lib
+    tail = tuple(gathered.shape[1:])
+    if out is None:
+        out = torch.empty((height,) + tail, dtype=gathered.dtype, device=gathered.device)
+    if tuple(out.shape) != (height,) + tail or out.dtype != gathered.dtype or out.device != gathered.device:
+        raise ValueError(f"frame tensor {tuple(out.shape)} {out.dtype} does not match {(height,) + tail} {gathered.dtype}")
+    if not (gathered[0].is_contiguous() and out[0].is_contiguous()):
+        raise ValueError("rows of the gathered buffer and the frame must be contiguous")
+    es = gathered.element_size()
+    st = torch.cuda.current_stream(gathered.device).cuda_stream
+    _lib.check(_lib.lib().rt_assemble_row_bands(
+        ctypes.c_void_p(gathered.data_ptr()), gathered.stride(0) * es, world, slot_rows, band_rows, height,
+        gathered[0].numel() * es, ctypes.c_void_p(out.data_ptr()), out.stride(0) * es, ctypes.c_void_p(st)))
+    return out
+
+
+def assemble_reference(gathered: torch.Tensor, height: int, world: int, layout: str, band: int,
+                       out: torch.Tensor = None) -> torch.Tensor:
+    """The same placement in torch ops.  Contiguous tiles are already in frame order (a view).
+    Cyclic slots hold bands g = b * world + rank at slot rows [b * band, (b + 1) * band), so the
+    frame is a permutation: view (world, bands_per_rank, band, ...) -> swap the first two axes ->
+    first H rows."""
     slot_rows = gathered.shape[0] // world
     if layout == "contiguous":
         frame = gathered[:height]

@@ -20,6 +20,7 @@ run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O
 run timeout -k 10 120 rocprofv3 -L > $OUT/${TAG}_counters.txt 2>&1 || true
 for PMC in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64" "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES" "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY" "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64"; do
   N=$(echo $PMC | tr ' ' '_' | cut -c1-40)
-  run timeout -k 10 300 rocprofv3 --pmc $PMC --output-format csv -d $OUT/${TAG}_pmc_$N -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/${TAG}_pmc_$N.err || echo "pmc pass $PMC failed (see $OUT/${TAG}_pmc_$N.err)"
+  # a failed or timed-out pass ends the session: nothing more runs on the GPU after it
+  run timeout -k 10 300 rocprofv3 --pmc $PMC --output-format csv -d $OUT/${TAG}_pmc_$N -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/${TAG}_pmc_$N.err || { echo "pmc pass $PMC failed (see $OUT/${TAG}_pmc_$N.err)"; exit 1; }
 done
 echo done
