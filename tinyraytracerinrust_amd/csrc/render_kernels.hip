@@ -27,6 +27,10 @@
 #include "rt_math.h"
 #include "scene.h"
 
+#ifdef RT_ABLATE_FAST_ACOS   // diagnostic cost-split builds only (wrong colours): acos in f32
+#define rt_acos(x) ((double)acosf((float)(x)))
+#endif
+
 #pragma clang fp contract(off)
 
 // Diagnostic section-cycle build (make profile-sections; never the product): wave-cycles spent
@@ -179,6 +183,10 @@ __device__ V3 leaf_normal(cptr<RtLeaf> L, V3 p, bool fin) {
 
 // MathSphere::get_uv_coordinates (:82-114): the centre is subtracted BEFORE the inverse transform
 __device__ void sphere_uv(cptr<RtLeaf> L, V3 p, double* u, double* v) {
+#ifdef RT_ABLATE_NO_UV       // diagnostic cost-split builds only (wrong colours)
+  *u = *v = 0.0;
+  if (p.x > 1e300) return;
+#endif
   V3 q = xf(L->inv, sub(p, ld3(L->c)));           // per shaded hit only: no short form
   q = scale(normalized(q), 1.0 - EPS);
   double phi = rt_acos(-((0.0 * q.x + 1.0 * q.y) + 0.0 * q.z));             // up = (0,1,0)
