@@ -19,9 +19,14 @@ L.rt_diag_cnt.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 buf = (ctypes.c_ulonglong * 32)()
 EV = ["rays", "obj box tests", "obj entered", "leaf box tests", "leaf evals", "  sphere", "  plane", "  cube",
       "filter calls"]
-for W, H, d in [(3840, 2160, 10), (3840, 2160, 0)]:
+# usage: event_counts.py [SCENE WxH TIME DEPTH[,DEPTH...]]   (default: globes 3840x2160 0 10,0)
+SCENE = sys.argv[1] if len(sys.argv) > 1 else "globes"
+W0, H0 = (int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "3840x2160").split("x"))
+TIME = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0
+DEPTHS = [int(v) for v in (sys.argv[4] if len(sys.argv) > 4 else "10,0").split(",")]
+for W, H, d in [(W0, H0, dd) for dd in DEPTHS]:
     rt = T.RayTracer(W, H)
-    rt.load_scene(open(os.path.join(S, "globes.scene")).read(), 0.0, asset_dir=S)
+    rt.load_scene(open(os.path.join(S, SCENE + ".scene")).read(), TIME, asset_dir=S)
     r = rt.renderer
     out = r.render_rows(0, H, max_depth=d)
     torch.cuda.synchronize()
@@ -29,7 +34,7 @@ for W, H, d in [(3840, 2160, 10), (3840, 2160, 0)]:
     r.render_rows(0, H, max_depth=d, out=out)
     torch.cuda.synchronize()
     L.rt_diag_cnt(buf)
-    print(f"globes {W}x{H} d={d}  (lane-events per frame; per-ray in brackets)")
+    print(f"{SCENE} {W}x{H} t={TIME:g} d={d}  (lane-events per frame; per-ray in brackets)")
     for c, nm in enumerate(["primary", "secondary", "shadow"]):
         rays = buf[c * 9] or 1
         print(f"  {nm}:")
