@@ -122,6 +122,7 @@ __device__ __forceinline__ bool wave_finite(V3 a) { return __ballot(!finite3(a))
 __device__ __forceinline__ bool wave_finite(V3 a, V3 b) { return __ballot(!(finite3(a) && finite3(b))) == 0; }
 // The leaf's inverse transform of a point (transformation.rs:53-59); `fin` = wave_finite(v).
 __device__ __forceinline__ V3 leaf_inv_xf(cptr<RtLeaf> L, V3 v, bool fin) {
+  if (L->xdiag == RT_XF_IDENTITY && fin) return v;
   if (L->xdiag && fin) return xf_diag(L->inv, v);
   return xf(L->inv, v);
 }
@@ -199,10 +200,16 @@ __device__ void sphere_uv(cptr<RtLeaf> L, V3 p, double* u, double* v) {
 
 // Candidate hit distances of one primitive for the world ray (ro, rd):
 // RTObject::intersects (rt_object.rs:28-31) = reverse_transform_ray + MathShape::intersects.
-// `fin` = wave_finite(ro, rd): selects the exact short form for diagonal-affine leaves.
+// `fin` = wave_finite(ro, rd): selects the exact short forms for identity / diagonal-affine
+// leaves (rt_blob.h).  POS: the caller accepts only t > EPS (the traversals), so a plane whose
+// distance is provably <= 0 from the signs alone skips its division (see the plane branch).
+template <bool POS = false>
 __device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, bool fin, double* t0, double* t1) {
   V3 o, d;
-  if (L->xdiag && fin) {                                                   // transformation.rs:88-93
+  if (L->xdiag == RT_XF_IDENTITY && fin) {
+    o = ro;
+    d = rd;
+  } else if (L->xdiag && fin) {                                            // transformation.rs:88-93
     o = xf_diag(L->inv, ro);
     d = sub(xf_diag(L->inv, rd), ld3(L->inv_o));
   } else {
@@ -226,7 +233,11 @@ __device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, boo
     V3 pn = ld3(L->pnorm);
     double v_d = dot(pn, d);
     if (v_d != 0.0) {
-      double t = -(dot(pn, o) + L->pl[0][3]) * (1.0 / v_d);
+      const double num = dot(pn, o) + L->pl[0][3];
+      // t = -num * (1/v_d) is > 0 only if num and v_d have opposite signs (rounding keeps signs;
+      // 1/v_d may overflow to +-inf, never to 0).  Otherwise t is <= 0, -0 or NaN: never > EPS.
+      if (POS && !((num > 0.0 && v_d < 0.0) || (num < 0.0 && v_d > 0.0))) return 0;
+      double t = -num * (1.0 / v_d);
       if (t >= 0.0) { *t0 = t; return 1; }
     }
     return 0;
@@ -369,7 +380,7 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
       CNT(cb + 4);
       CNT(cb + 5 + (L->kind == RT_N_SPHERE ? 0 : L->kind == RT_N_PLANE ? 1 : 2));
       double t0 = 0.0, t1 = 0.0;
-      int n = leaf_candidates(L, ro, rd, fin, &t0, &t1);
+      int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1);
       const bool filtered = L->prog_end != L->prog_begin;
       if (filtered && ((n >= 1 && t0 > EPS && t0 < best) || (n >= 2 && t1 > EPS))) CNT(cb + 8);
       if (n >= 1 && t0 > EPS && t0 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) {
@@ -424,7 +435,7 @@ __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
       CNT(cb + 4);
       CNT(cb + 5 + (L->kind == RT_N_SPHERE ? 0 : L->kind == RT_N_PLANE ? 1 : 2));
       double t0 = 0.0, t1 = 0.0;
-      int n = leaf_candidates(L, p, dir, fin, &t0, &t1);
+      int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1);
       const bool filtered = L->prog_end != L->prog_begin;
       if (filtered && ((n >= 1 && t0 > EPS && t0 < dist) || (n >= 2 && t1 > EPS && t1 < dist))) CNT(cb + 8);
       if (n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) {

@@ -49,6 +49,8 @@ enum RtProgOp : int32_t {
 
 struct RtProg { int32_t op, arg; };
 
+#define RT_XF_IDENTITY 2   // RtLeaf::xdiag value of an identity inverse (a diagonal-affine special case)
+
 struct alignas(16) RtLeaf {
   double inv[12];       // inverse matrix rows 0..2 (row-major, 4 per row)
   double inv_o[3];      // transform_vector((0,0,0), inverse)   (transformation.rs:80-83)
@@ -70,7 +72,8 @@ struct alignas(16) RtLeaf {
   int32_t prog_begin;   // hit-filter program [prog_begin, prog_end)
   int32_t prog_end;
   int32_t cull;         // RtCull
-  int32_t xdiag;        // inv is diagonal-affine (see below): transform_vector has a 2-op form
+  int32_t xdiag;        // 1: inv is diagonal-affine (see below): transform_vector has a 2-op form;
+                        // RT_XF_IDENTITY: inv is the identity and inv_o = 0: no transform at all
   int32_t n_lit;        // >= 0: the filter program is the conjunction of n_lit literals below
   int32_t lit[RT_MAX_LITS];   // literal = 2 * leaf + want: leaf[lit >> 1].is_inside(p) == (lit & 1)
   int32_t pad[2];
@@ -87,7 +90,9 @@ struct alignas(16) RtLeaf {
 // the other components; a zero distance is rejected by `d > EPS` (and compares equal either way
 // in the ortho views); a zero direction component takes the `dir == 0` branch of the cube slab
 // test for both signs.  The kernel takes the short form only when every input of the wave is
-// finite (0 * inf would be NaN in the full form).
+// finite (0 * inf would be NaN in the full form).  RT_XF_IDENTITY (diagonal entries exactly 1,
+// translations and inv_o exactly +-0) is the same argument once more: 1 * x + (+-0) = x up to the
+// sign of a zero, and a direction minus inv_o = +-0 likewise, so the transform is skipped.
 
 struct RtNode {
   int32_t kind;         // RtNodeKind

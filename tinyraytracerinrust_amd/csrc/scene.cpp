@@ -137,7 +137,9 @@ static void leaf_common(const rt_transformation& t, RtLeaf* L) {
       if (!std::isfinite(v)) diag = false;
       if (j < 3 && j != i && v != 0.0) diag = false;
     }
-  L->xdiag = diag ? 1 : 0;
+  const bool ident = diag && m[0] == 1.0 && m[5] == 1.0 && m[10] == 1.0 && m[3] == 0.0 && m[7] == 0.0 &&
+                     m[11] == 0.0 && io.x == 0.0 && io.y == 0.0 && io.z == 0.0;
+  L->xdiag = ident ? RT_XF_IDENTITY : diag ? 1 : 0;
 }
 
 // MathPlane::new (math_shapes.rs:140-152): raw (a,b,c,d) + transformed unit normal.
