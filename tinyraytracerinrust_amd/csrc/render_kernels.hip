@@ -92,7 +92,11 @@ struct DS {                         // device view of RtDevScene
 };
 
 constexpr double EPS = RT_EPSILON;
-#define RT_LIGHT_GROUP 4            // shadow transparencies held in registers per light group
+#ifndef RT_LIGHT_GROUP
+#define RT_LIGHT_GROUP 1            // shadow transparencies held in registers per light group: 1 frees
+                                    // the registers that let reflection-only scenes run 7 waves/SIMD
+                                    // (profiles/r01ad_ab_light_group.txt)
+#endif
 constexpr double PI_D = 3.14159265358979323846;   // std::f64::consts::PI
 
 struct V3 { double x, y, z; };
@@ -813,9 +817,18 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
 //   y = y_first + (r / band_rows) * band_pitch + r % band_rows
 // (a contiguous tile [y0, y1) is one band; the cyclic multi-GPU layout deals bands of
 // band_rows rows with pitch world * band_rows).  Workgroup = 16x16 output pixels, wave = 8x8.
+// Waves per SIMD (VGPR budget 512 / N) per instantiation: reflection-only scenes (REFR = false)
+// run 7 (<= 72 VGPRs; with RT_LIGHT_GROUP 1: 7.4 % faster than 5 waves on 4K globes, 8 waves
+// spills and is 23 % slower), refraction scenes keep 4 (128 VGPRs: their deeper frame state
+// spills at 5, 1.6-3.5 % slower on spinning_globes), profiles/r01ac_ab_sched.txt,
+// profiles/r01ad_ab_light_group.txt.
 #ifndef RT_WAVES_PER_EU
-#define RT_WAVES_PER_EU 4   // 128 VGPRs: measured best (profiles/r01_occupancy_sweep.txt)
+#define RT_WAVES_PER_EU 4
 #endif
+#ifndef RT_WAVES_PER_EU_NOREFR
+#define RT_WAVES_PER_EU_NOREFR 7
+#endif
+#define RT_WAVES(REFR) ((REFR) ? RT_WAVES_PER_EU : RT_WAVES_PER_EU_NOREFR)
 // Workgroup = RT_WG_WX x RT_WG_WY waves of 8x8 pixels.
 #ifndef RT_WG_WX
 #define RT_WG_WX 1          // one wave per workgroup: measured 3-5% faster than 2x2 (r01q)
@@ -826,7 +839,7 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
 constexpr int RT_WG_THREADS = 64 * RT_WG_WX * RT_WG_WY;
 constexpr int RT_TILE_W = 8 * RT_WG_WX, RT_TILE_H = 8 * RT_WG_WY;
 template <bool REFR, bool F64>
-__global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU))) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
+__global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(RT_WAVES(REFR)))) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
                                                           int n_rows, int max_depth, uint8_t* __restrict__ out,
                                                           size_t stride) {
 #ifdef RT_DIAG_LDS                       // diagnostic builds only: cap occupancy with an LDS pad
