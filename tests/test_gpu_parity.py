@@ -227,3 +227,26 @@ def test_assemble_row_bands_kernel(T, W, world, band):
     assert torch.equal(padded.cpu(), want)
     with pytest.raises(T.RtError):                                      # slot too small for the layout
         D._assemble_device(g[: world * (slot_rows - band)], H, world, slot_rows - band, band)
+
+
+@pytest.mark.parametrize("scene,time,W,H,depth", [("globes", 0.25, 160, 120, 10),
+                                                   ("spinning_globes", 0.1, 160, 120, 10)])
+def test_cost_ordered_dispatch_parity(T, scene, time, W, H, depth):
+    """The first launch of a geometry on a context records every tile's wave time (row-major
+    dispatch); later launches dispatch the tiles longest-first (DESIGN.md "Tile order").  Every
+    launch must give the oracle's bits."""
+    from oracle import oracle as O
+    rt = T.RayTracer(W, H)
+    rt.max_depth = depth
+    rt.load_scene(scene_text(scene), time, asset_dir=SCENES)
+    r = rt.renderer
+    u8 = [r.render_rows_host(0, H) for _ in range(3)]          # calibrate, then ordered twice
+    f = [r.render_rows_host(0, H, f64=True) for _ in range(2)]
+    assert np.array_equal(u8[0], u8[1]) and np.array_equal(u8[1], u8[2])
+    assert np.array_equal(f[0], f[1], equal_nan=True)
+    ref_f, ref_u8 = O.OracleScene(scene_text(scene), time, W, H, max_depth=depth).render(0, H, f64=True)
+    assert_close(u8[2], f[1], ref_u8, ref_f, f"{scene} t={time} ordered")
+    # a new scene on the same context measures again
+    rt.load_scene(scene_text(scene), time + 0.125, asset_dir=SCENES)
+    a, b = rt.renderer.render_rows_host(0, H), rt.renderer.render_rows_host(0, H)
+    assert np.array_equal(a, b)

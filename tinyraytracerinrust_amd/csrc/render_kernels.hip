@@ -15,6 +15,8 @@
 // A = parent.intensify(1 - w) -- exactly the `final.intensify(1-w) + R.intensify(w)` of
 // raytracer.rs:256-257 / :278-279.
 #include <hip/hip_runtime.h>
+#include <algorithm>
+#include <stdlib.h>
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
@@ -838,17 +840,24 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
 #endif
 constexpr int RT_WG_THREADS = 64 * RT_WG_WX * RT_WG_WY;
 constexpr int RT_TILE_W = 8 * RT_WG_WX, RT_TILE_H = 8 * RT_WG_WY;
-template <bool REFR, bool F64>
+template <bool REFR, bool F64, bool CAL = false>
 __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(RT_WAVES(REFR)))) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
                                                           int n_rows, int max_depth, uint8_t* __restrict__ out,
-                                                          size_t stride) {
+                                                          size_t stride, const int32_t* __restrict__ order,
+                                                          uint32_t* __restrict__ cost) {
 #ifdef RT_DIAG_LDS                       // diagnostic builds only: cap occupancy with an LDS pad
   __shared__ volatile char rt_pad[RT_DIAG_LDS];
   if (threadIdx.x == 0) rt_pad[0] = 0;
 #endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tiles_x = (S.width + RT_TILE_W - 1) / RT_TILE_W;
-  const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
+  // Tile dispatch order (see launch_bands): `order` lists the tiles most expensive first, as
+  // measured on a calibration launch that stored each tile's wave time in `cost`.
+  // CAL (the calibration instantiation) is the only one that carries the timing code.
+  const unsigned tile = CAL || !order ? blockIdx.x : (unsigned)order[blockIdx.x];
+  [[maybe_unused]] uint64_t t_start = 0;
+  if constexpr (CAL) t_start = wall_clock64();
+  const unsigned tiles_x = (unsigned)(S.width + RT_TILE_W - 1) / RT_TILE_W;
+  const int bx = (int)(tile % tiles_x), by = (int)(tile / tiles_x);
   const int x = bx * RT_TILE_W + (wave % RT_WG_WX) * 8 + (lane & 7);
   const int r = by * RT_TILE_H + (wave / RT_WG_WX) * 8 + (lane >> 3);
   if (x >= S.width || r >= n_rows) return;
@@ -872,6 +881,8 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   } else {
     ((uint32_t*)row)[x] = to_u8(c.r) | (to_u8(c.g) << 8) | (to_u8(c.b) << 16) | (255u << 24);
   }
+  if constexpr (CAL)
+    if (threadIdx.x == 0) cost[tile] = (uint32_t)(wall_clock64() - t_start);   // vector store
 }
 
 template <bool REFR>
@@ -1194,6 +1205,14 @@ struct rt_ctx {
   bool timed = false;
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  // Cost-ordered tile dispatch.  A frame's time is set by its slowest tiles (long reflection
+  // chains), so they are dispatched first: the first launch of a geometry records every tile's
+  // wave time, and later launches of the same geometry read the tiles in descending cost order.
+  int32_t* d_order = nullptr;
+  uint32_t* d_cost = nullptr;
+  size_t order_cap = 0;               // tiles the two buffers hold
+  bool order_valid = false;
+  int32_t ok[7] = {0};                // geometry the order was measured for
 };
 
 using rt::fail;
@@ -1203,6 +1222,18 @@ using rt::fail;
     hipError_t e_ = (call);                                                            \
     if (e_ != hipSuccess) return fail(RT_ERR_DEVICE, "%s failed: %s", #call, hipGetErrorString(e_)); \
   } while (0)
+
+#ifndef RT_ORDER_RUN
+#define RT_ORDER_RUN 1                // tiles per sorted run: 1 measured best (profiles/r01ah_tile_order_sweep.txt)
+#endif
+// RT_TILE_ORDER=0 in the environment turns the cost-ordered dispatch off (row-major tiles).
+static bool tile_order_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RT_TILE_ORDER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 static int ensure_scratch(rt_ctx* c, size_t bytes) {
   if (c->scratch_bytes >= bytes) return RT_OK;
@@ -1317,6 +1348,7 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   d.cam = f.cam;
   c->max_depth = f.max_depth;
   c->uploaded = true;
+  c->order_valid = false;
   return RT_OK;
 }
 
@@ -1349,15 +1381,76 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   const int tiles_x = (c->dev.width + RT_TILE_W - 1) / RT_TILE_W, tiles_y = (int)((n_rows + RT_TILE_H - 1) / RT_TILE_H);
   dim3 grid((unsigned)(tiles_x * tiles_y)), block(RT_WG_THREADS);
   const int a0 = (int)y_first, a1 = (int)band_rows, a2 = (int)band_pitch, a3 = (int)n_rows;
+  // Tile order: reuse the measured order for this exact geometry, else calibrate on this launch.
+  const size_t n_tiles = (size_t)tiles_x * (size_t)tiles_y;
+  const int32_t key[7] = {a0, a1, a2, a3, max_depth, f64 ? 1 : 0, c->dev.width};
+  const bool use_order = tile_order_enabled() && c->order_valid && memcmp(key, c->ok, sizeof(key)) == 0;
+  bool calibrate = false;
+  if (!use_order && tile_order_enabled()) {
+    if (c->order_cap < n_tiles) {
+      if (c->d_order) (void)hipFree(c->d_order);
+      if (c->d_cost) (void)hipFree(c->d_cost);
+      c->d_order = nullptr; c->d_cost = nullptr; c->order_cap = 0; c->order_valid = false;
+      RT_HIP(hipMalloc((void**)&c->d_order, n_tiles * sizeof(int32_t)));
+      RT_HIP(hipMalloc((void**)&c->d_cost, n_tiles * sizeof(uint32_t)));
+      c->order_cap = n_tiles;
+    }
+    calibrate = true;
+  }
+  const int32_t* order = use_order ? c->d_order : nullptr;
+  uint32_t* cost = calibrate ? c->d_cost : nullptr;
   RT_HIP(hipEventRecord(c->ev0, st));
   const bool refr = c->dev.any_transparent != 0;
-  if (refr && f64) hipLaunchKernelGGL((render_rows_kernel<true, true>), grid, block, 0, st, c->dev, a0, a1, a2, a3, max_depth, target, tstride);
-  else if (refr) hipLaunchKernelGGL((render_rows_kernel<true, false>), grid, block, 0, st, c->dev, a0, a1, a2, a3, max_depth, target, tstride);
-  else if (f64) hipLaunchKernelGGL((render_rows_kernel<false, true>), grid, block, 0, st, c->dev, a0, a1, a2, a3, max_depth, target, tstride);
-  else hipLaunchKernelGGL((render_rows_kernel<false, false>), grid, block, 0, st, c->dev, a0, a1, a2, a3, max_depth, target, tstride);
+#define RT_LAUNCH_ROWS(R, F)                                                                                  \
+  if (calibrate) hipLaunchKernelGGL((render_rows_kernel<R, F, true>), grid, block, 0, st, c->dev, a0, a1, a2, a3, \
+                                    max_depth, target, tstride, order, cost);                                   \
+  else hipLaunchKernelGGL((render_rows_kernel<R, F, false>), grid, block, 0, st, c->dev, a0, a1, a2, a3,         \
+                          max_depth, target, tstride, order, cost);
+  if (refr && f64) { RT_LAUNCH_ROWS(true, true) }
+  else if (refr) { RT_LAUNCH_ROWS(true, false) }
+  else if (f64) { RT_LAUNCH_ROWS(false, true) }
+  else { RT_LAUNCH_ROWS(false, false) }
+#undef RT_LAUNCH_ROWS
   RT_HIP(hipGetLastError());
   RT_HIP(hipEventRecord(c->ev1, st));
   c->timed = true;
+  if (calibrate) {                    // synchronous, once per geometry and scene upload
+    std::vector<uint32_t> h_cost(n_tiles);
+    std::vector<int32_t> h_order(n_tiles);
+    RT_HIP(hipMemcpyAsync(h_cost.data(), c->d_cost, n_tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    RT_HIP(hipStreamSynchronize(st));
+    // Longest-first: sort runs of RT_ORDER_RUN horizontally adjacent tiles (env RT_ORDER_RUN
+    // overrides) by their summed cost, each run's tiles kept consecutive.  With runs of 1 every
+    // tile is placed by its own cost; longer runs keep neighbours together (measured slower).
+    static const int run_env = [] { const char* e = getenv("RT_ORDER_RUN"); return e ? atoi(e) : 0; }();
+    const int run = run_env > 0 ? run_env : RT_ORDER_RUN, runs_x = (tiles_x + run - 1) / run;
+    const size_t n_runs = (size_t)runs_x * (size_t)tiles_y;
+    std::vector<uint64_t> run_cost(n_runs, 0);
+    std::vector<int32_t> run_order(n_runs);
+    for (size_t t = 0; t < n_tiles; ++t)
+      run_cost[(t / tiles_x) * runs_x + (t % tiles_x) / run] += h_cost[t];
+    for (size_t i = 0; i < n_runs; ++i) run_order[i] = (int32_t)i;
+    std::stable_sort(run_order.begin(), run_order.end(), [&](int32_t x, int32_t y) { return run_cost[x] > run_cost[y]; });
+    size_t k = 0;
+    for (int32_t rr : run_order) {
+      const int ty = rr / runs_x, tx0 = (rr % runs_x) * run;
+      for (int tx = tx0; tx < tx0 + run && tx < tiles_x; ++tx) h_order[k++] = ty * tiles_x + tx;
+    }
+    if (getenv("RT_TILE_ORDER_IDENTITY"))   // diagnostic: the table without the reordering
+      for (size_t i = 0; i < n_tiles; ++i) h_order[i] = (int32_t)i;
+    RT_HIP(hipMemcpyAsync(c->d_order, h_order.data(), n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    RT_HIP(hipStreamSynchronize(st));
+    memcpy(c->ok, key, sizeof(key));
+    c->order_valid = true;
+    if (getenv("RT_TILE_ORDER_DEBUG")) {    // wave times in wall-clock ticks (100 MHz)
+      std::vector<uint32_t> v(h_cost);
+      std::sort(v.begin(), v.end());
+      double sum = 0.0;
+      for (uint32_t x : v) sum += x;
+      fprintf(stderr, "tile order: %zu tiles, max %u, p99 %u, p90 %u, median %u, mean %.1f ticks\n", n_tiles, v.back(),
+              v[n_tiles * 99 / 100], v[n_tiles * 9 / 10], v[n_tiles / 2], sum / n_tiles);
+    }
+  }
   if (!dev_out) {
     RT_HIP(hipMemcpy2DAsync(out, stride, target, tstride, row_bytes, n_rows, hipMemcpyDeviceToHost, st));
     RT_HIP(hipStreamSynchronize(st));
@@ -1650,6 +1743,8 @@ void rt_ctx_free(rt_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   if (c->d_blob) (void)hipFree(c->d_blob);
   if (c->scratch) (void)hipFree(c->scratch);
+  if (c->d_order) (void)hipFree(c->d_order);
+  if (c->d_cost) (void)hipFree(c->d_cost);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
