@@ -8,6 +8,7 @@
   (gfx950 tallies 128-B read requests at 64 B); both counters are KB per dispatch.
 """
 import csv
+import re
 import glob
 import json
 import os
@@ -28,7 +29,11 @@ def main(tag="r01", config="globes4k", kernel="render_rows_kernel"):
     agg = defaultdict(list)
     for f in glob.glob(os.path.join(out, f"{tag}_pmc_*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if kernel in r["Kernel_Name"]:
+            # the product instantiation only: render_rows_kernel<REFR, F64, CAL=false>; the one
+            # calibration launch per geometry (CAL=true, "...ELb1EEEv") is excluded
+            m = re.search(r"render_rows_kernel<([^>]*)>", r["Kernel_Name"])
+            cal = m is not None and len(m.group(1).split(",")) == 3 and m.group(1).split(",")[2].strip() == "true"
+            if kernel in r["Kernel_Name"] and not cal:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     mean = {k: sum(v) / len(v) for k, v in agg.items()}
     res = {"kernel": kernel, "dispatches_per_counter": {k: len(v) for k, v in agg.items()}, "mean": mean}
