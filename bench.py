@@ -72,7 +72,7 @@ def parse():
                     help="exercise the N > 1 path (process group, bands, all-gather) even at N = 1")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=2,
                     help="anim120: frames dealt round-robin over this many HIP streams so independent "
                          "frames' kernels overlap (one 1080p frame does not fill the GPU to its end)")
     ap.add_argument("--png", default="", help="write the rendered frame (rank 0) to this PNG")
