@@ -72,6 +72,9 @@ def parse():
                     help="exercise the N > 1 path (process group, bands, all-gather) even at N = 1")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="N > 1: frames whose band renders may overlap, each on its own HIP stream (a rank's "
+                         "share is floored by its slowest tile, so one frame alone leaves the GPU idle)")
     ap.add_argument("--streams", type=int, default=2,
                     help="anim120: frames dealt round-robin over this many HIP streams so independent "
                          "frames' kernels overlap (one 1080p frame does not fill the GPU to its end)")
@@ -175,42 +178,51 @@ def main():
     frame = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     overlap = multi and not a.no_overlap
-    # N > 1: double-buffered slot / gather buffers so frame k's all-gather (RCCL stream) runs
-    # under frame k+1's render (compute stream); every frame is still fully assembled.
-    nbuf = 2 if overlap else 1
+    # N > 1: frame k's all-gather (RCCL stream) runs under later frames' renders, and up to
+    # `inflight` frames' band renders overlap, each frame on its own HIP stream: a rank's share
+    # of the frame is floored by its slowest tile (DESIGN.md "Multi-GPU"), so a lone frame
+    # leaves the GPU idle.  Every frame is still fully rendered, gathered and assembled.
+    K = max(1, a.inflight) if overlap else 1
+    nbuf = K + 1 if overlap else 1
+    rstreams = [stream] if K == 1 else [torch.cuda.Stream(dev) for _ in range(K)]
     slots = [torch.zeros((slot_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
     gath = [torch.zeros((world * slot_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
     frames = [frame] + [torch.zeros_like(frame) for _ in range(nbuf - 1)]
-    pending = [None]           # (work, buffer index) of the gather not yet assembled
+    free_ev = [None] * nbuf    # buffer b's last gather and assembly are done once this event fires
+    pending = []               # (work, buffer, stream) of gathers not yet assembled, oldest first
 
     def finish(p):
-        work, b = p
-        work.wait()
-        D.assemble(gath[b], H, world, layout, band, out=frames[b])
+        work, b, s = p
+        with torch.cuda.stream(s):
+            work.wait()                                   # s waits for the gather
+            D.assemble(gath[b], H, world, layout, band, out=frames[b])
+            free_ev[b] = torch.cuda.Event()
+            free_ev[b].record(s)
 
     def step(i, ev0=None, ev1=None):
         b = i % nbuf
-        if ev0 is not None:
-            ev0.record(stream)
-        if not multi:
-            rend.render_rows(0, H, max_depth=depth, out=frame, stream=stream)
-        else:
-            rend.render_row_bands(y_first, band_rows, pitch, n_bands, slots[b], max_depth=depth, stream=stream)
-        if ev1 is not None:
-            ev1.record(stream)
+        s = rstreams[i % K]
+        with torch.cuda.stream(s):
+            if free_ev[b] is not None:
+                s.wait_event(free_ev[b])                  # slot / gather / frame buffers reusable
+            if ev0 is not None:
+                ev0.record(s)
+            if not multi:
+                rend.render_rows(0, H, max_depth=depth, out=frame, stream=s)
+            else:
+                rend.render_row_bands(y_first, band_rows, pitch, n_bands, slots[b], max_depth=depth, stream=s)
+            if ev1 is not None:
+                ev1.record(s)
+            if multi:
+                work = dist.all_gather_into_tensor(gath[b], slots[b], async_op=True)   # after s's render
         if multi:
-            work = dist.all_gather_into_tensor(gath[b], slots[b], async_op=True)
-            if pending[0] is not None:
-                finish(pending[0])
-            pending[0] = (work, b)
-            if not overlap:
-                finish(pending[0])
-                pending[0] = None
+            pending.append((work, b, s))
+            while len(pending) > (K if overlap else 0):
+                finish(pending.pop(0))
 
     def drain():
-        if pending[0] is not None:
-            finish(pending[0])
-            pending[0] = None
+        while pending:
+            finish(pending.pop(0))
 
     for i in range(a.warmup):
         step(i)
@@ -234,6 +246,14 @@ def main():
         elapsed = float(e.item())
     kernel_ms = [s.elapsed_time(e) for s, e in evs]
     mean_kernel_ms = sum(kernel_ms) / len(kernel_ms)
+    if multi:
+        # outside the timed region: the last assembled frame must equal this rank's own
+        # single-launch render of the whole frame (catches any stream-ordering mistake)
+        whole = rend.render_rows(0, H, max_depth=depth)
+        torch.cuda.synchronize(dev)
+        if not torch.equal(frames[(a.warmup + a.steps - 1) % nbuf], whole):
+            raise SystemExit(f"rank {rank}: assembled frame differs from the single-launch render")
+    busy_ms = mean_kernel_ms if K == 1 else elapsed * 1e3 / a.steps
 
     if rank == 0 and a.png:
         T.write_png(a.png, frames[(a.warmup + a.steps - 1) % nbuf].cpu().numpy())
@@ -246,7 +266,7 @@ def main():
     rows_rendered = [y for (y0, y1) in mine for y in range(y0, y1)]
     fl = load_flops(scene, W, H, t, depth)
     flops_launch = sum(fl["row_flops"][y] for y in rows_rendered) if fl else None
-    achieved = flops_launch / (mean_kernel_ms * 1e-3) / 1e12 if flops_launch else None
+    achieved = flops_launch / (busy_ms * 1e-3) / 1e12 if flops_launch else None
     traffic = load_traffic(a.config, world, layout)
     # algorithmic bytes of one launch: its RGBA8 rows written + scene blob + the texture once
     alg_bytes = len(rows_rendered) * W * 4 + 1024 * 568 * 4 + 16 * 1024
@@ -270,7 +290,8 @@ def main():
                         + f" {W}x{H} t={t:g} max_depth {depth}, one frame per step",
             "scene": f"{scene}.scene" if scene == "globes" else SPHERE_SCENE, "width": W, "height": H, "time": t, "max_depth": depth,
             "parallelism": f"rowtile{world}" + ("" if not multi else f"-{layout}" + (f"{band}" if layout == "cyclic" else "")),
-            "collective": None if not multi else "all_gather_into_tensor (RCCL)" + (", overlapped with next frame" if overlap else ""),
+            "collective": None if not multi else "all_gather_into_tensor (RCCL)" + (
+                f", overlapped with later frames; {K} frame(s) in flight on HIP streams" if overlap else ""),
             "frame_bytes": W * H * 4,
         },
         "roofline": {
@@ -282,6 +303,7 @@ def main():
             "traffic": traffic,
             "kernel": "render_rows_kernel",
             "kernel_ms_mean": round(mean_kernel_ms, 4),
+            "achieved_basis": "kernel event time" if K == 1 else f"step wall time ({K} frames in flight)",
             "kernel_ms_min": round(min(kernel_ms), 4),
             "algorithmic_flops_per_launch": flops_launch,
             "frac_of_no_fma_ceiling": round(achieved / FP64_NO_FMA_TFLOPS, 4) if achieved else None,
@@ -289,10 +311,10 @@ def main():
         },
         "roofline_hbm": {
             "bound": "hbm",
-            "achieved": round(alg_bytes / (mean_kernel_ms * 1e-3) / 1e9, 2),
+            "achieved": round(alg_bytes / (busy_ms * 1e-3) / 1e9, 2),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(alg_bytes / (mean_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "frac": round(alg_bytes / (busy_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
             "algorithmic_bytes_per_launch": alg_bytes,
             "traffic": traffic,
         },
