@@ -25,13 +25,24 @@ HBM).  rank 0 prints ONE JSON line with two extra objects:
   (profiles/) when it exists for this workload, else null.  ``roofline_hbm`` restates the same
   launch against HBM bandwidth, as the north star asks.
 * cpu_baseline -- the CPU oracle (a faithful C restatement of the reference loop; the Rust
-  reference cannot be built here) timed on this host on rank 0 at N=1 only.
+  reference cannot be built here) timed on this host on rank 0 at N=1 only, on every core this
+  process may run on (sched_getaffinity, capped by the cgroup CPU quota), as the reference's
+  threadpool is sized to num_cpus (src/raydebugger/gui.rs:49-51), plus a 1-thread sample.
+
+Launching: ``python bench.py --gpus N`` with N > 1 outside torch.distributed.run starts N rank
+processes itself (a torch.distributed.run child, before this process touches the GPU) and exits
+with its status; rank 0's JSON line is the child's stdout.  ``--launcher-check`` runs the same
+N-rank machinery on CPU under gloo with a synthetic per-pixel pattern instead of rendering (no
+GPU, no measurement): band layout, all-gather and assembly are checked (tests/test_bench_launcher.py).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -70,7 +81,8 @@ def parse():
                     help="N > 1: do not overlap frame k's all-gather with frame k+1's render")
     ap.add_argument("--force-collective", action="store_true",
                     help="exercise the N > 1 path (process group, bands, all-gather) even at N = 1")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0 = every core available to this process)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=2,
                     help="N > 1: frames whose band renders may overlap, each on its own HIP stream (a rank's "
@@ -79,7 +91,54 @@ def parse():
                     help="anim120: frames dealt round-robin over this many HIP streams so independent "
                          "frames' kernels overlap (one 1080p frame does not fill the GPU to its end)")
     ap.add_argument("--png", default="", help="write the rendered frame (rank 0) to this PNG")
+    ap.add_argument("--launcher-check", action="store_true",
+                    help="CPU/gloo check of the N-rank launcher, band layout, all-gather and assembly with a "
+                         "synthetic pixel pattern (no GPU, no rendering, no measurement)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(a) -> int:
+    """N > 1 without a launcher: run N ranks under torch.distributed.run as a CHILD process (this
+    process has not touched the GPU) and return its exit status.  Rank 0's stdout -- the one JSON
+    line -- is inherited."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def host_cpus():
+    """(cores this process may use, CPU model, affinity count, cgroup quota or None)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    cores = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return min(cores, 256), model, aff, quota
 
 
 def owned_rows(H, world, rank, layout, band):
@@ -108,9 +167,11 @@ def load_traffic(config, world, layout):
 
 
 def cpu_baseline(text, W, H, t, depth, threads, target_s=1.0):
-    """Time the CPU oracle: all `threads` on whole frames (repeated until ~target_s of wall time,
-    i.e. ~16 thread-s of CPU work at 16 threads), and 1 thread on a row sample."""
+    """Time the CPU oracle: `threads` threads (default: every available core) on whole frames,
+    repeated until ~target_s of wall time (at least one frame), and 1 thread on a row sample."""
     from oracle import oracle as O
+    cores, model, aff, quota = host_cpus()
+    threads = threads or cores
     O.register_texture_file("worldmap.png", os.path.join(SCENES, "worldmap.png"))
     sc = O.OracleScene(text, t, W, H, max_depth=depth)
     frames = 0
@@ -131,6 +192,9 @@ def cpu_baseline(text, W, H, t, depth, threads, target_s=1.0):
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
+        "cpu_model": model,
+        "host_cpus_affinity": aff,
+        "cgroup_cpu_quota": quota,
         "sample": f"{frames} whole {W}x{H} frame(s), rows interleaved over {threads} threads "
                   f"({dt_all * frames * threads:.1f} thread-s of CPU work); oracle/rt_oracle.c -O2 -ffp-contract=off",
         "single_thread_value": round(rows * W / dt_one / 1e6, 3),
@@ -140,10 +204,15 @@ def cpu_baseline(text, W, H, t, depth, threads, target_s=1.0):
 
 def main():
     a = parse()
+    launched = "WORLD_SIZE" in os.environ or "LOCAL_RANK" in os.environ
+    if a.gpus > 1 and not launched:
+        sys.exit(self_launch(a))         # before anything here touches the GPU
     # Exactly one JSON line on stdout: libraries (RCCL prints a version banner at communicator
     # creation) write to fd 1 as well, so route fd 1 to stderr and keep a private copy for the line.
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    if a.launcher_check:
+        return launcher_check(a, json_out)
     import torch
     import torch.distributed as dist
     import tinyraytracerinrust_amd as T
@@ -153,8 +222,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: one rank per GPU")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     multi = world > 1 or a.force_collective
@@ -246,13 +314,22 @@ def main():
         elapsed = float(e.item())
     kernel_ms = [s.elapsed_time(e) for s, e in evs]
     mean_kernel_ms = sum(kernel_ms) / len(kernel_ms)
+    frame_check = None
+    rows_per_rank = None
     if multi:
-        # outside the timed region: the last assembled frame must equal this rank's own
-        # single-launch render of the whole frame (catches any stream-ordering mistake)
+        # outside the timed region: every frame buffer holds one of the last assembled frames,
+        # each must equal this rank's own single-launch render of the whole frame (catches any
+        # stream-ordering or buffer-reuse mistake)
         whole = rend.render_rows(0, H, max_depth=depth)
         torch.cuda.synchronize(dev)
-        if not torch.equal(frames[(a.warmup + a.steps - 1) % nbuf], whole):
-            raise SystemExit(f"rank {rank}: assembled frame differs from the single-launch render")
+        used = min(nbuf, a.warmup + a.steps)
+        bad = [b for b in range(used) if not torch.equal(frames[b], whole)]
+        if bad:
+            raise SystemExit(f"rank {rank}: assembled frame buffer(s) {bad} differ from the single-launch render")
+        frame_check = f"all {used} assembled frame buffers == single-launch render, on every rank"
+        counts = [None] * world
+        dist.all_gather_object(counts, sum(y1 - y0 for y0, y1 in mine))
+        rows_per_rank = counts
     busy_ms = mean_kernel_ms if K == 1 else elapsed * 1e3 / a.steps
 
     if rank == 0 and a.png:
@@ -294,6 +371,7 @@ def main():
                 f", overlapped with later frames; {K} frame(s) in flight on HIP streams" if overlap else ""),
             "frame_bytes": W * H * 4,
         },
+        "rays": rays_line(fl, W * H * a.steps / elapsed),
         "roofline": {
             "bound": "fp64-valu",
             "achieved": round(achieved, 3) if achieved else None,
@@ -320,6 +398,10 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if multi:
+        line["distributed"] = {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(),
+                               "rows_per_rank": rows_per_rank, "layout": layout, "band_rows": band,
+                               "frames_in_flight": K, "frame_check": frame_check}
     if world == 1 and not multi and not a.no_cpu_baseline:
         cb = cpu_baseline(text, W, H, t, depth, a.cpu_threads)
         cb["gpu_over_cpu"] = round(line["value"] / cb["value"], 1)
@@ -328,6 +410,70 @@ def main():
     json_out.flush()
     if multi:
         dist.destroy_process_group()
+
+
+def rays_line(fl, primary_per_s):
+    """Primary + shadow + reflection + refraction rays of one frame, from the oracle's counters
+    (the same ray definition as the reference's spawn sites, raytracer.rs:176,243,268)."""
+    if not fl or "totals" not in fl:
+        return None
+    t = fl["totals"]
+    n = {k: int(t.get("ray_" + k, 0)) for k in ("primary", "shadow", "reflect", "refract")}
+    total = sum(n.values())
+    frames = fl.get("frames", 1)
+    return {"per_frame": {k: v // frames for k, v in n.items()}, "total_per_frame": total // frames,
+            "total_Mrays_s": round(primary_per_s * total / n["primary"] / 1e6, 2) if n["primary"] else None,
+            "source": "oracle event counters (tests/golden/flops_*.json)"}
+
+
+def launcher_check(a, json_out):
+    """The N-rank machinery without a GPU: gloo process group, this rank's band layout filled the
+    way rt_render_row_bands fills it (output row r -> frame row y_first + (r / band_rows) *
+    band_pitch + r % band_rows) with a per-pixel pattern, one all_gather_into_tensor, the frame
+    assembly, and a check of the assembled frame on every rank."""
+    import torch
+    import torch.distributed as dist
+    from tinyraytracerinrust_amd import distributed as D
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dist.init_process_group("gloo")
+    W, H = 97, 163                                   # odd sizes: padded slots, partial last band
+    layout = a.layout
+    band = a.band if layout == "cyclic" else -(-H // world)
+
+    def pattern(ys):
+        ys = torch.as_tensor(ys, dtype=torch.int64).view(-1, 1).expand(-1, W)
+        xs = torch.arange(W, dtype=torch.int64).view(1, -1).expand(len(ys), -1)
+        return torch.stack([ys & 255, ys >> 8, xs & 255, xs >> 8], -1).to(torch.uint8)
+
+    slot_rows = D.rows_per_rank(H, world, layout, band)
+    y_first, band_rows, pitch, n_bands = D.band_params(H, world, rank, layout, band)
+    slot = torch.zeros((slot_rows, W, 4), dtype=torch.uint8)
+    ys = [y_first + (r // band_rows) * pitch + r % band_rows for r in range(band_rows * n_bands)] if band_rows else []
+    keep = [r for r, y in enumerate(ys) if y < H]
+    if keep:
+        slot[keep] = pattern([ys[r] for r in keep])
+    ok = True
+    for _ in range(max(1, a.steps)):
+        gath = torch.empty((world * slot_rows, W, 4), dtype=torch.uint8)
+        dist.all_gather_into_tensor(gath, slot)
+        frame = D.assemble(gath, H, world, layout, band)
+        ok = ok and torch.equal(frame, pattern(range(H)))
+    flags = [None] * world
+    dist.all_gather_object(flags, (ok, len(keep)))
+    if rank == 0:
+        line = {"metric": "launcher check (synthetic pattern, no rendering, no measurement)", "value": None,
+                "n_gpus": world, "steps": a.steps, "warmup": 0,
+                "distributed": {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(),
+                                "rows_per_rank": [n for _, n in flags], "layout": layout, "band_rows": band,
+                                "frame_check": all(f for f, _ in flags)},
+                "config": {"width": W, "height": H}}
+        json_out.write(json.dumps(line) + "\n")
+        json_out.flush()
+    dist.destroy_process_group()
+    if not all(f for f, _ in flags):
+        sys.exit(1)
 
 
 def anim_main(a, json_out, rank, world, local, dev, multi):
@@ -435,20 +581,23 @@ def anim_main(a, json_out, rank, world, local, dev, multi):
             "kernel_ms_max": round(max(per_frame), 4),
             "frac_of_no_fma_ceiling": round(achieved / FP64_NO_FMA_TFLOPS, 4) if achieved else None,
         },
+        "rays": rays_line(fl, F * W * H * a.steps / elapsed),
         "host_compile_upload_ms_per_frame": round(prep_ms, 3),
         "cpu_baseline": None,
     }
     if world == 1 and not multi and not a.no_cpu_baseline:
         from oracle import oracle as O
+        cores, model, aff, quota = host_cpus()
+        threads = a.cpu_threads or cores
         sample = list(range(0, F, 30))
         t0 = time.perf_counter()
         for f in sample:
-            O.OracleScene(text, f / F, W, H, max_depth=depth).render(0, H, threads=a.cpu_threads, u8=True)
+            O.OracleScene(text, f / F, W, H, max_depth=depth).render(0, H, threads=threads, u8=True)
         dt = time.perf_counter() - t0
-        cb = {"value": round(len(sample) * W * H / dt / 1e6, 3), "unit": "Mrays/s", "cores": a.cpu_threads,
-              "kind": "port",
-              "sample": f"frames {sample} (whole frames, rows interleaved over {a.cpu_threads} threads, "
-                        f"{dt * a.cpu_threads:.1f} thread-s); oracle/rt_oracle.c -O2 -ffp-contract=off"}
+        cb = {"value": round(len(sample) * W * H / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads,
+              "kind": "port", "cpu_model": model, "host_cpus_affinity": aff, "cgroup_cpu_quota": quota,
+              "sample": f"frames {sample} (whole frames, rows interleaved over {threads} threads, "
+                        f"{dt * threads:.1f} thread-s); oracle/rt_oracle.c -O2 -ffp-contract=off"}
         cb["gpu_over_cpu"] = round(line["value"] / cb["value"], 1)
         line["cpu_baseline"] = cb
     json_out.write(json.dumps(line) + "\n")

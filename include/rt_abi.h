@@ -148,10 +148,13 @@ int rt_ctx_upload(rt_ctx* ctx, const rt_scene* scene);
  * `(c * 255.0) as u8` (easy_pixbuf.rs:49-52), R,G,B,A order.  rgba8 may be a device pointer
  * (written by the kernel on `stream`, asynchronously) or a host pointer (rendered into the
  * context's scratch and copied back; synchronous).  max_depth < 0 uses the scene's.
- * Tile order: the first launch of a row geometry (rows, bands, depth, f64) on a context after
- * rt_ctx_upload also records every 8x8 tile's time and returns only after the host has sorted
- * the tiles (synchronous, once); later launches of that geometry dispatch the costliest tiles
- * first.  The pixels are identical either way.  RT_TILE_ORDER=0 in the environment disables it. */
+ * Tile order: the first launch of a row geometry (rows, bands, depth, f64) of >= 2048 8x8 tiles
+ * on a context after rt_ctx_upload also records every tile's time and returns only after the
+ * host has sorted the tiles (synchronous, once per geometry); later launches of that geometry
+ * dispatch the costliest tiles first.  A context keeps the orders of its 8 most recently used
+ * geometries; an order table is written once and never rewritten while launches on any stream
+ * may read it.  Smaller launches are dispatched row-major.  The pixels are identical either
+ * way.  RT_TILE_ORDER=0 in the environment disables it. */
 int rt_render_rows(rt_ctx* ctx, uint32_t y0, uint32_t y1, int32_t max_depth,
                    uint8_t* rgba8, size_t row_stride_bytes, void* stream);
 /* Band layout for multi-GPU row tiling: n_bands bands of band_rows rows, band b covering

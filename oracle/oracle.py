@@ -35,12 +35,25 @@ COUNTER_NAMES = [
 _libs: dict = {}
 
 
+def usable_cores() -> int:
+    """Cores this process may run on: the affinity mask, capped by the cgroup CPU quota (a GPU
+    box's os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                n = min(n, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def default_threads() -> int:
-    """Host threads for oracle renders: the CPU share of a GPU box is 16 (os.cpu_count() there
-    reports the whole machine), here it is 8."""
-    n = os.cpu_count() or 1
+    """Host threads for oracle renders (tests, smoke): every usable core, at most 64, or
+    $ORACLE_THREADS."""
     env = os.environ.get("ORACLE_THREADS")
-    return int(env) if env else max(1, min(16, n))
+    return int(env) if env else min(64, usable_cores())
 _registered: dict = {}
 
 

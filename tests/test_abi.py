@@ -91,3 +91,27 @@ def test_no_gpu_fails_loudly():
     with pytest.raises(T.RtError) as e:
         T.Renderer(0)
     assert e.value.status == -5
+
+
+def _header_arity():
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(rt_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", src, flags=re.S):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_integration_rust_block_matches_header():
+    """INTEGRATION.md's Rust `extern "C"` block declares every header export with the same
+    number of parameters (the binding a Rust maintainer would paste)."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    blocks = re.findall(r'extern "C" \{(.*?)\n\}', doc, flags=re.S)
+    assert blocks, "no extern block"
+    rust = {}
+    for m in re.finditer(r"pub fn (rt_[a-z0-9_]+)\s*\((.*?)\)\s*(->[^;]*)?;", blocks[0], flags=re.S):
+        args = re.sub(r"//[^\n]*", "", m.group(2)).strip()
+        rust[m.group(1)] = 0 if not args else args.rstrip(",").count(",") + 1
+    hdr = _header_arity()
+    assert sorted(hdr) == declared()
+    assert rust == hdr

@@ -1,0 +1,43 @@
+"""bench.py's N-rank launcher on CPU: ``python bench.py --gpus N`` started WITHOUT
+torch.distributed.run must start its own N ranks (as the driver may launch it), and each rank
+must own its band layout, all-gather it and assemble the frame.  ``--launcher-check`` runs that
+machinery under gloo with a per-pixel pattern in place of the renderer (the reference's row loop
+being tiled is src/raydebugger/debug_window.rs:74-87)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from tests.conftest import ROOT
+
+
+def _run(*args):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       env=env, timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout           # exactly one JSON line, from rank 0
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world,layout", [(2, "cyclic"), (2, "contiguous"), (3, "cyclic")])
+def test_self_launch_gloo(world, layout):
+    line = _run("--gpus", str(world), "--launcher-check", "--layout", layout, "--steps", "2")
+    d = line["distributed"]
+    assert line["n_gpus"] == world
+    assert d["world_size_seen"] == world and d["backend"] == "gloo"
+    assert d["frame_check"] is True
+    assert len(d["rows_per_rank"]) == world and sum(d["rows_per_rank"]) == line["config"]["height"]
+
+
+def test_host_cpus_reports_usable_cores():
+    sys.path.insert(0, ROOT)
+    import bench
+    cores, model, aff, quota = bench.host_cpus()
+    assert 1 <= cores <= aff
+    assert isinstance(model, str) and model

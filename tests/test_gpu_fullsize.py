@@ -1,0 +1,97 @@
+"""Full-frame parity at every BASELINE configuration's real size (BASELINE.json configs 2-5):
+every pixel of the HIP render, through the C ABI, against the CPU oracle (a restatement of
+src/raytracer/raytracer.rs:132-287 and its callees) on all usable host cores.
+
+* 3840x2160 globes.scene, depth 10: the calibration launch (row-major, records tile costs) AND the
+  cost-ordered launch that follows it;
+* 1920x1080 globes.scene, depth 5;
+* 1920x1080 single sphere, depth 0 (config 2);
+* 8 frames spread over the 120-frame spinning_globes animation at 1920x1080, time = f / 120;
+* the DSL-quirk scenes of tests/test_oracle.py compiled by the PRODUCT's rt_scene_compile and
+  rendered on the GPU.
+
+Bar: RGBA8 within 1 LSB per channel (north star), >= 99.99 % of channels exact; the frames are
+expected bit-identical (the count of differing channels is printed).  These pin the exactness of
+the kernels' culling (render_kernels.hip "conservative culling") over whole frames.
+"""
+import numpy as np
+import pytest
+
+from tests.conftest import SCENES, scene_text
+from tests.test_gpu_parity import assert_close
+
+pytestmark = pytest.mark.gpu
+
+SPHERE = "draw(sphere(<0, 0, 0>, 30, red))"
+
+
+@pytest.fixture(scope="module")
+def T():
+    import torch
+    import tinyraytracerinrust_amd as T
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return T
+
+
+def gpu_frames(T, text, time, W, H, depth, launches=2):
+    """`launches` whole-frame renders on one context into device buffers (the first of a
+    geometry of >= 2048 tiles is the calibration launch, later ones are cost-ordered)."""
+    import torch
+    rt = T.RayTracer(W, H)
+    rt.max_depth = depth
+    rt.load_scene(text, time, asset_dir=SCENES)
+    out = []
+    for _ in range(launches):
+        f = rt.renderer.render_rows(0, H)
+        torch.cuda.synchronize()
+        out.append(f.cpu().numpy())
+    return out
+
+
+def oracle_frame(text, time, W, H, depth):
+    from oracle import oracle as O
+    _, u8 = O.OracleScene(text, time, W, H, max_depth=depth).render(0, H)
+    return u8
+
+
+@pytest.mark.parametrize("name,text,W,H,depth", [
+    ("globes4k_d10", "globes", 3840, 2160, 10),
+    ("globes1080_d5", "globes", 1920, 1080, 5),
+    ("sphere1080_d0", None, 1920, 1080, 0),
+])
+def test_baseline_config_full_frame(T, worldmap, name, text, W, H, depth):
+    text = scene_text(text) if text else SPHERE
+    cal, ordered = gpu_frames(T, text, 0.0, W, H, depth)
+    ref = oracle_frame(text, 0.0, W, H, depth)
+    assert_close(cal, None, ref, None, f"{name} calibration launch")
+    assert_close(ordered, None, ref, None, f"{name} ordered launch")
+    print(f"{name}: {int((cal != ref).sum())} / {ref.size} channels differ (calibration), "
+          f"{int((ordered != ref).sum())} (ordered)")
+    assert (ordered[..., 3] == 255).all()
+
+
+@pytest.mark.parametrize("frame", list(range(0, 120, 15)))
+def test_spinning_globes_animation_frames(T, frame):
+    """BASELINE config 5: frame f of 120 at time f / 120, 1920x1080, depth 10 (refraction)."""
+    text = scene_text("spinning_globes")
+    W, H = 1920, 1080
+    cal, ordered = gpu_frames(T, text, frame / 120, W, H, 10)
+    ref = oracle_frame(text, frame / 120, W, H, 10)
+    assert_close(cal, None, ref, None, f"spinning_globes f={frame} calibration launch")
+    assert_close(ordered, None, ref, None, f"spinning_globes f={frame} ordered launch")
+
+
+def test_dsl_quirk_scenes_through_product_compiler(T):
+    """The DSL-quirk cases (operator-chain dropping, locals/globals, while, camera transformed
+    twice, default arguments, appended lights, ...) compiled by rt_scene_compile and rendered by
+    the HIP kernels, against the oracle's own parse + render of the same text."""
+    from tests.test_oracle import DSL_CASES
+    from oracle import oracle as O
+    W, H = 160, 120
+    for key, text in sorted(DSL_CASES.items()):
+        rt = T.RayTracer(W, H)
+        rt.load_scene(text, 0.0, asset_dir=SCENES)
+        gu = rt.renderer.render_rows_host(0, H)
+        gf = rt.renderer.render_rows_host(0, H, f64=True)
+        rf, ru = O.OracleScene(text, 0.0, W, H).render(0, H, f64=True)
+        assert_close(gu, gf, ru, rf, f"DSL {key}")

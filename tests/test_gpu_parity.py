@@ -250,3 +250,28 @@ def test_cost_ordered_dispatch_parity(T, scene, time, W, H, depth):
     rt.load_scene(scene_text(scene), time + 0.125, asset_dir=SCENES)
     a, b = rt.renderer.render_rows_host(0, H), rt.renderer.render_rows_host(0, H)
     assert np.array_equal(a, b)
+
+
+def test_tile_orders_of_interleaved_geometries_on_two_streams(T):
+    """Launches of different row geometries queued on two streams of one context, with new
+    geometries calibrated while earlier launches are still queued: every frame must equal the
+    synchronous render (an order table is never rewritten while a launch may read it)."""
+    import torch
+    W, H = 640, 480                                  # 4800 tiles: cost-ordered dispatch is on
+    rt = T.RayTracer(W, H)
+    rt.load_scene(scene_text("globes"), 0.0, asset_dir=SCENES)
+    r = rt.renderer
+    geoms = [(0, H, 10), (0, H, 5), (0, H - 8, 10), (8, H, 4)]
+    want = {g: r.render_rows_host(g[0], g[1], max_depth=g[2]) for g in geoms}
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    rt2 = T.RayTracer(W, H)                         # a fresh context: every geometry calibrates here
+    rt2.load_scene(scene_text("globes"), 0.0, asset_dir=SCENES)
+    r2 = rt2.renderer
+    outs = []
+    for it in range(3):
+        for k, g in enumerate(geoms):
+            s = s1 if (k + it) % 2 == 0 else s2
+            outs.append((g, r2.render_rows(g[0], g[1], max_depth=g[2], stream=s)))
+    torch.cuda.synchronize()
+    for g, o in outs:
+        assert np.array_equal(o.cpu().numpy(), want[g]), f"geometry {g}"

@@ -1208,11 +1208,21 @@ struct rt_ctx {
   // Cost-ordered tile dispatch.  A frame's time is set by its slowest tiles (long reflection
   // chains), so they are dispatched first: the first launch of a geometry records every tile's
   // wave time, and later launches of the same geometry read the tiles in descending cost order.
-  int32_t* d_order = nullptr;
-  uint32_t* d_cost = nullptr;
-  size_t order_cap = 0;               // tiles the two buffers hold
-  bool order_valid = false;
-  int32_t ok[7] = {0};                // geometry the order was measured for
+  // One table per geometry key (rows, bands, depth, f64, width), RT_ORDER_SLOTS of them, LRU.
+  // A table is written exactly once (its calibration, synchronous) and never rewritten while it
+  // exists, so launches queued on other streams can never read a half-written order; tables are
+  // freed only by hipFree (which waits for the device) on eviction, upload or rt_ctx_free.
+  struct OrderSlot {
+    int32_t key[7] = {0};
+    int32_t* d_order = nullptr;
+    uint32_t* d_cost = nullptr;
+    size_t n_tiles = 0;
+    uint64_t last_use = 0;
+    bool valid = false;               // set once the sorted order is on the device
+  };
+  static constexpr int RT_ORDER_SLOTS = 8;
+  OrderSlot order[RT_ORDER_SLOTS];
+  uint64_t use_clock = 0;
 };
 
 using rt::fail;
@@ -1234,6 +1244,22 @@ static bool tile_order_enabled() {
   }();
   return on;
 }
+
+static void drop_order(rt_ctx::OrderSlot& s) {
+  if (s.d_order) (void)hipFree(s.d_order);     // hipFree waits for work that may still read it
+  if (s.d_cost) (void)hipFree(s.d_cost);
+  s = rt_ctx::OrderSlot();
+}
+static void drop_orders(rt_ctx* c) {
+  for (auto& s : c->order) drop_order(s);
+}
+
+// Launches with fewer tiles than this are dispatched row-major without a calibration launch: a
+// small band (a single row, one rank's sliver) has no tail worth reordering, and calibrating it
+// would cost a host synchronisation per new geometry.
+#ifndef RT_ORDER_MIN_TILES
+#define RT_ORDER_MIN_TILES 2048
+#endif
 
 static int ensure_scratch(rt_ctx* c, size_t bytes) {
   if (c->scratch_bytes >= bytes) return RT_OK;
@@ -1348,7 +1374,7 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   d.cam = f.cam;
   c->max_depth = f.max_depth;
   c->uploaded = true;
-  c->order_valid = false;
+  drop_orders(c);                     // tile costs belong to the previous scene
   return RT_OK;
 }
 
@@ -1384,21 +1410,29 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   // Tile order: reuse the measured order for this exact geometry, else calibrate on this launch.
   const size_t n_tiles = (size_t)tiles_x * (size_t)tiles_y;
   const int32_t key[7] = {a0, a1, a2, a3, max_depth, f64 ? 1 : 0, c->dev.width};
-  const bool use_order = tile_order_enabled() && c->order_valid && memcmp(key, c->ok, sizeof(key)) == 0;
+  rt_ctx::OrderSlot* slot = nullptr;
   bool calibrate = false;
-  if (!use_order && tile_order_enabled()) {
-    if (c->order_cap < n_tiles) {
-      if (c->d_order) (void)hipFree(c->d_order);
-      if (c->d_cost) (void)hipFree(c->d_cost);
-      c->d_order = nullptr; c->d_cost = nullptr; c->order_cap = 0; c->order_valid = false;
-      RT_HIP(hipMalloc((void**)&c->d_order, n_tiles * sizeof(int32_t)));
-      RT_HIP(hipMalloc((void**)&c->d_cost, n_tiles * sizeof(uint32_t)));
-      c->order_cap = n_tiles;
+  if (tile_order_enabled() && n_tiles >= RT_ORDER_MIN_TILES) {
+    for (auto& s : c->order)
+      if (s.valid && memcmp(s.key, key, sizeof(key)) == 0) slot = &s;
+    if (!slot) {                      // calibrate into the empty or least recently used slot
+      slot = &c->order[0];
+      for (auto& s : c->order) {
+        if (!s.valid) { slot = &s; break; }
+        if (s.last_use < slot->last_use) slot = &s;
+      }
+      drop_order(*slot);
+      RT_HIP(hipMalloc((void**)&slot->d_order, n_tiles * sizeof(int32_t)));
+      RT_HIP(hipMalloc((void**)&slot->d_cost, n_tiles * sizeof(uint32_t)));
+      RT_HIP(hipMemsetAsync(slot->d_cost, 0, n_tiles * sizeof(uint32_t), st));   // tiles that store no cost sort last
+      memcpy(slot->key, key, sizeof(key));
+      slot->n_tiles = n_tiles;
+      calibrate = true;
     }
-    calibrate = true;
+    slot->last_use = ++c->use_clock;
   }
-  const int32_t* order = use_order ? c->d_order : nullptr;
-  uint32_t* cost = calibrate ? c->d_cost : nullptr;
+  const int32_t* order = slot && !calibrate ? slot->d_order : nullptr;
+  uint32_t* cost = calibrate ? slot->d_cost : nullptr;
   RT_HIP(hipEventRecord(c->ev0, st));
   const bool refr = c->dev.any_transparent != 0;
 #define RT_LAUNCH_ROWS(R, F)                                                                                  \
@@ -1417,7 +1451,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   if (calibrate) {                    // synchronous, once per geometry and scene upload
     std::vector<uint32_t> h_cost(n_tiles);
     std::vector<int32_t> h_order(n_tiles);
-    RT_HIP(hipMemcpyAsync(h_cost.data(), c->d_cost, n_tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    RT_HIP(hipMemcpyAsync(h_cost.data(), slot->d_cost, n_tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     RT_HIP(hipStreamSynchronize(st));
     // Longest-first: sort runs of RT_ORDER_RUN horizontally adjacent tiles (env RT_ORDER_RUN
     // overrides) by their summed cost, each run's tiles kept consecutive.  With runs of 1 every
@@ -1438,10 +1472,9 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     }
     if (getenv("RT_TILE_ORDER_IDENTITY"))   // diagnostic: the table without the reordering
       for (size_t i = 0; i < n_tiles; ++i) h_order[i] = (int32_t)i;
-    RT_HIP(hipMemcpyAsync(c->d_order, h_order.data(), n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    RT_HIP(hipMemcpyAsync(slot->d_order, h_order.data(), n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, st));
     RT_HIP(hipStreamSynchronize(st));
-    memcpy(c->ok, key, sizeof(key));
-    c->order_valid = true;
+    slot->valid = true;
     if (getenv("RT_TILE_ORDER_DEBUG")) {    // wave times in wall-clock ticks (100 MHz)
       std::vector<uint32_t> v(h_cost);
       std::sort(v.begin(), v.end());
@@ -1743,8 +1776,7 @@ void rt_ctx_free(rt_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   if (c->d_blob) (void)hipFree(c->d_blob);
   if (c->scratch) (void)hipFree(c->scratch);
-  if (c->d_order) (void)hipFree(c->d_order);
-  if (c->d_cost) (void)hipFree(c->d_cost);
+  drop_orders(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;

@@ -23,12 +23,15 @@ def main():
     ap.add_argument("--time", type=float, default=0.0)
     ap.add_argument("--depth", type=int, default=10)
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--text", default="",
+                    help="scene text instead of tests/golden/scenes/<scene>.scene (e.g. BASELINE config 2's one-line "
+                         "sphere scene, written as flops_sphere_*.json with --scene sphere)")
     ap.add_argument("--frames", type=int, default=0,
                     help="animation mode: per-frame totals of frames f = 0..F-1 at time f/F (BASELINE config 5)")
     a = ap.parse_args()
     scenes = os.path.join(ROOT, "tests", "golden", "scenes")
     O.register_texture_file("worldmap.png", os.path.join(scenes, "worldmap.png"))
-    text = open(os.path.join(scenes, a.scene + ".scene")).read()
+    text = a.text or open(os.path.join(scenes, a.scene + ".scene")).read()
     if a.frames:
         return animation(a, text)
     sc = O.OracleScene(text, a.time, a.width, a.height, max_depth=a.depth, counting=True)
@@ -39,7 +42,7 @@ def main():
         for k, v in c.items():
             totals[k] = totals.get(k, 0) + v
     out = {
-        "scene": a.scene + ".scene", "width": a.width, "height": a.height, "time": a.time,
+        "scene": a.text or a.scene + ".scene", "width": a.width, "height": a.height, "time": a.time,
         "max_depth": a.depth, "flop_definition": "f64 add/sub/mul/div/sqrt and libm acos/sin calls as the "
         "reference evaluates them (oracle/rt_oracle.c FL/TR); negation, comparisons, clamps not counted",
         "totals": totals, "row_flops": rows,
