@@ -84,8 +84,11 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0 = every core available to this process)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="N > 1: frames whose band renders may overlap, each on its own HIP stream (a rank's "
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="frames whose renders may overlap, each on its own HIP stream (0 = 1 at N = 1, so the "
+                         "roofline's kernel time is one launch alone; 4 at N > 1, profiles/r02f_inflight.txt).  A "
+                         "frame's tail is its costliest "
+                         "tiles, so a lone frame leaves the GPU partly idle at its end (a rank's "
                          "share is floored by its slowest tile, so one frame alone leaves the GPU idle)")
     ap.add_argument("--streams", type=int, default=2,
                     help="anim120: frames dealt round-robin over this many HIP streams so independent "
@@ -246,12 +249,15 @@ def main():
     frame = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     overlap = multi and not a.no_overlap
-    # N > 1: frame k's all-gather (RCCL stream) runs under later frames' renders, and up to
-    # `inflight` frames' band renders overlap, each frame on its own HIP stream: a rank's share
-    # of the frame is floored by its slowest tile (DESIGN.md "Multi-GPU"), so a lone frame
-    # leaves the GPU idle.  Every frame is still fully rendered, gathered and assembled.
-    K = max(1, a.inflight) if overlap else 1
-    nbuf = K + 1 if overlap else 1
+    # Up to K frames' renders overlap, each frame on its own HIP stream: a frame (or a rank's
+    # share of it) ends with its costliest tiles running alone (DESIGN.md "Multi-GPU"), so a lone
+    # frame leaves the GPU partly idle.  N > 1: frame k's all-gather (RCCL stream) also runs under
+    # later frames' renders.  Every frame is still fully rendered (gathered and assembled) inside
+    # the timed region.
+    K = a.inflight if a.inflight > 0 else (1 if world == 1 else 4)
+    if multi and not overlap:
+        K = 1
+    nbuf = K + 1 if multi else K     # N = 1: buffer b is only ever written on stream b
     rstreams = [stream] if K == 1 else [torch.cuda.Stream(dev) for _ in range(K)]
     slots = [torch.zeros((slot_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
     gath = [torch.zeros((world * slot_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
@@ -276,7 +282,7 @@ def main():
             if ev0 is not None:
                 ev0.record(s)
             if not multi:
-                rend.render_rows(0, H, max_depth=depth, out=frame, stream=s)
+                rend.render_rows(0, H, max_depth=depth, out=frames[b], stream=s)
             else:
                 rend.render_row_bands(y_first, band_rows, pitch, n_bands, slots[b], max_depth=depth, stream=s)
             if ev1 is not None:
@@ -314,19 +320,18 @@ def main():
         elapsed = float(e.item())
     kernel_ms = [s.elapsed_time(e) for s, e in evs]
     mean_kernel_ms = sum(kernel_ms) / len(kernel_ms)
-    frame_check = None
     rows_per_rank = None
+    # outside the timed region: every frame buffer holds one of the last frames (assembled, at
+    # N > 1); each must equal a single-launch render of the whole frame on the default stream
+    # (catches any stream-ordering or buffer-reuse mistake)
+    whole = rend.render_rows(0, H, max_depth=depth)
+    torch.cuda.synchronize(dev)
+    used = min(nbuf, a.warmup + a.steps)
+    bad = [b for b in range(used) if not torch.equal(frames[b], whole)]
+    if bad:
+        raise SystemExit(f"rank {rank}: frame buffer(s) {bad} differ from the single-launch render")
+    frame_check = f"all {used} frame buffers == single-launch render" + (", on every rank" if multi else "")
     if multi:
-        # outside the timed region: every frame buffer holds one of the last assembled frames,
-        # each must equal this rank's own single-launch render of the whole frame (catches any
-        # stream-ordering or buffer-reuse mistake)
-        whole = rend.render_rows(0, H, max_depth=depth)
-        torch.cuda.synchronize(dev)
-        used = min(nbuf, a.warmup + a.steps)
-        bad = [b for b in range(used) if not torch.equal(frames[b], whole)]
-        if bad:
-            raise SystemExit(f"rank {rank}: assembled frame buffer(s) {bad} differ from the single-launch render")
-        frame_check = f"all {used} assembled frame buffers == single-launch render, on every rank"
         counts = [None] * world
         dist.all_gather_object(counts, sum(y1 - y0 for y0, y1 in mine))
         rows_per_rank = counts
@@ -368,7 +373,8 @@ def main():
             "scene": f"{scene}.scene" if scene == "globes" else SPHERE_SCENE, "width": W, "height": H, "time": t, "max_depth": depth,
             "parallelism": f"rowtile{world}" + ("" if not multi else f"-{layout}" + (f"{band}" if layout == "cyclic" else "")),
             "collective": None if not multi else "all_gather_into_tensor (RCCL)" + (
-                f", overlapped with later frames; {K} frame(s) in flight on HIP streams" if overlap else ""),
+                ", overlapped with later frames" if overlap else ""),
+            "frames_in_flight": K,
             "frame_bytes": W * H * 4,
         },
         "rays": rays_line(fl, W * H * a.steps / elapsed),
@@ -397,6 +403,7 @@ def main():
             "traffic": traffic,
         },
         "cpu_baseline": None,
+        "frame_check": frame_check,
     }
     if multi:
         line["distributed"] = {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(),

@@ -1,0 +1,48 @@
+"""The deferred-shadow path (render_kernels.hip trace_deferred: chain phase, wave-wide shadow
+phase through an LDS window, post-order fold) on EVERY tile -- RT_DEFERRED=1, which the library
+reads once per process, so the check runs in a child process -- against the oracle
+(src/raytracer/raytracer.rs:132-287): small frames (no ordered launch, lanes outside the frame
+trace other lanes' shadow rays) and ordered frames whose costliest tiles are split over several
+waves."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from tests.conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+CHILD = r"""
+import sys
+sys.path.insert(0, ROOT)
+import numpy as np
+import tinyraytracerinrust_amd as T
+from oracle import oracle as O
+from tests.conftest import SCENES, scene_text
+O.register_texture_file("worldmap.png", SCENES + "/worldmap.png")
+cases = [("globes", 0.0, 64, 48, 10), ("globes", 0.25, 161, 121, 10), ("globes", 0.0, 640, 480, 10),
+         ("globes", 0.5, 640, 480, 3), ("three_cubes", 0.0, 160, 120, 10), ("spinning_cube", 0.3, 160, 120, 10),
+         ("ground_star", 0.2, 160, 120, 10), ("spinning_gimbals", 0.4, 160, 120, 10), ("fractal", 0.0, 96, 72, 10)]
+for name, t, W, H, d in cases:
+    rt = T.RayTracer(W, H)
+    rt.max_depth = d
+    rt.load_scene(scene_text(name), t, asset_dir=SCENES)
+    frames = [rt.renderer.render_rows_host(0, H) for _ in range(2)]     # calibration (if ordered), ordered
+    f64 = rt.renderer.render_rows_host(0, H, f64=True)
+    rf, ru = O.OracleScene(scene_text(name), t, W, H, max_depth=d).render(0, H, f64=True)
+    for u in frames:
+        assert np.array_equal(u, ru), (name, t, W, H, int((u != ru).sum()))
+    assert np.nanmax(np.abs(f64 - rf)) <= 1e-9, name
+    print("ok", name, t, W, H, d, flush=True)
+"""
+
+
+def test_every_tile_on_the_deferred_path():
+    env = dict(os.environ, RT_DEFERRED="1")
+    p = subprocess.run([sys.executable, "-c", f"ROOT = {ROOT!r}\n" + CHILD], env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=240)
+    print(p.stdout)
+    assert p.returncode == 0, p.stderr[-4000:]
+    assert p.stdout.count("ok ") == 9

@@ -528,6 +528,16 @@ __device__ Col texture_color(const DS& S, int tex, double u, double v) {
   return {(double)(px & 0xffu) / 255.0, (double)((px >> 8) & 0xffu) / 255.0, (double)((px >> 16) & 0xffu) / 255.0};
 }
 
+// angle(-dir, n) >= PI/2 (raytracer.rs:230-231) from the cosine `cin` the angle's acos would take
+// (vector.rs:57-59).  acos is monotone and rt_acos is within 1 ulp, so for |cin| > 1e-15 (>= 4 ulp
+// of PI/2 away from the threshold) the sign decides exactly -- except past -1: a cosine that
+// rounds below -1 (a ray through a sphere's centre meets the normal head-on) makes acos NaN and
+// the comparison false, so such a hit is NOT inside.  Near-grazing cosines (and NaN) evaluate
+// the acos itself.
+__device__ __forceinline__ bool inside_test(double cin) {
+  return cin < -1e-15 ? cin >= -1.0 : (cin > 1e-15 ? false : rt_acos(cin) >= PI_D / 2.0);
+}
+
 __device__ __forceinline__ V3 reflect_dir(V3 i, V3 n) {                    // raytracer.rs:332-334
   return sub(i, scale(scale(n, 2.0), dot(n, i)));
 }
@@ -718,11 +728,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
       C = {0.0, 0.0, 0.0};                                               // Color::BLACK (:152-160)
     } else {
       const V3 nd = scale(rd, -1.0);                                      // :230-235
-      // angle(-dir, n) >= PI/2 (:230-231).  acos is monotone and rt_acos is within 1 ulp, so for
-      // |cos| > 1e-15 (>= 4 ulp of PI/2 away from the threshold) the sign of the cosine decides
-      // exactly; only near-grazing hits (and NaN) evaluate the acos itself.
-      const double cin = dot(nd, nrm) / (len(nd) * len(nrm));
-      const bool inside = cin < -1e-15 ? true : (cin > 1e-15 ? false : rt_acos(cin) >= PI_D / 2.0);
+      const bool inside = inside_test(dot(nd, nrm) / (len(nd) * len(nrm)));
       const V3 n2 = inside ? scale(nrm, -1.0) : nrm;
       const double r1 = inside ? 1.45 : 1.0, r2 = inside ? 1.0 : 1.45;
       bool tir = false;
@@ -788,6 +794,158 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
     }
     if (!descend) return C;
   }
+}
+
+// ---------------------------------------------------------------- deferred shadows (REFR=false)
+// get_ray_color (raytracer.rs:132-287) for scenes without a transparent object, restructured so
+// a pixel's critical path is its chain of nearest hits rather than nearest hits AND every shadow
+// ray in series.  Without refraction every hit spawns at most one ray (the reflection), so a
+// pixel's rays form a chain and the reference's recursion computes
+//     C_h = L_h                                            (no reflection spawned)
+//     C_h = in_range(in_range(L_h * (1 - w_h)) + in_range(C_{h+1} * w_h))      (:267-280)
+// with L_h = the ambient + per-light Lambert terms of hit h (:172-228) and C = BLACK for a ray
+// that misses (:152-160).  Every L_h is a pure function of hit h and its lights' shadow
+// transparencies, so the three steps run as phases of one wave:
+//   1. chain:   per lane, trace the nearest-hit chain; per hit record p, the normal, the material
+//               colour and the reflection weight w in the lane's arrays (every hit but possibly
+//               the last spawned a reflection);
+//   2. shadows: every (hit, light) shadow ray of the WHOLE WAVE is dealt densely over its 64
+//               lanes through an LDS window (one round = up to 64 hits; the hits' owners write
+//               their points, any lane traces any (hit, light) pair, the owners read the
+//               transparencies back and form L_h in light order, :199-227);
+//   3. fold:    per lane, C from the last hit back to the first, the post-order combine.
+// Same operations, same order per value: bit-identical to trace<false>.  A pixel whose chain is
+// 11 bounces long now waits for 11 nearest-hit traversals plus a few dense shadow rounds, not
+// 11 * (1 + lights) serial traversals; lanes whose chains ended early trace other lanes' shadow
+// rays instead of idling.
+#ifndef RT_SH_TRCAP
+#define RT_SH_TRCAP 128             // shadow results per round: hits per round = min(64, TRCAP / lights)
+#endif
+#define RT_SPLIT_TILE_MASK 0xFFFFFu   // order entries: tile index in bits 0-19 (split tiles: see below)
+struct ShadowWin {                  // LDS, one per wave: 2.5 KB
+  double px[64], py[64], pz[64];
+  double tr[RT_SH_TRCAP];
+};
+
+#ifdef RT_TILE_STATS                // diagnostic build only: per-tile phase times and chain lengths
+#define RT_STATS_TILES (1 << 18)
+__device__ uint32_t g_tile_stats[RT_STATS_TILES][4];
+#endif
+
+template <int HC>
+__device__ Col trace_deferred(const DS& S, V3 ro, V3 rd, int max_depth, bool valid, ShadowWin* win,
+                              [[maybe_unused]] int stats_tile = -1) {
+#ifdef RT_TILE_STATS
+  const uint64_t ts0 = wall_clock64();
+  int rounds = 0;
+#endif
+  double hP[HC][3], hN[HC][3], hC[HC][3], hW[HC];
+  int nh = 0;
+  bool last_spawned = false;          // the last hit spawned a reflection ray (that missed)
+  // ---- phase 1: the nearest-hit chain
+  if (valid) {
+    for (int depth = 0;; ++depth) {
+      double t_hit;
+      const int oi = nearest_hit(S, ro, rd, &t_hit, depth == 0 ? 0 : 1);
+      if (oi < 0) break;                                                   // BLACK (:152-160)
+      const V3 p = add(ro, scale(rd, t_hit));                               // :162
+      V3 nrm;
+      Col c;
+      double transp, refl;
+      shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);                    // :163-170
+      // inside test (:230-235), exactly as trace(); no transparent object: no refraction, no TIR
+      const V3 nd = scale(rd, -1.0);
+      const bool inside = inside_test(dot(nd, nrm) / (len(nd) * len(nrm)));
+      const bool do_refl = depth < max_depth && refl != 0.0 && !inside;    // :267
+      hP[nh][0] = p.x; hP[nh][1] = p.y; hP[nh][2] = p.z;
+      hN[nh][0] = nrm.x; hN[nh][1] = nrm.y; hN[nh][2] = nrm.z;
+      hC[nh][0] = c.r; hC[nh][1] = c.g; hC[nh][2] = c.b;
+      hW[nh] = refl;
+      ++nh;
+      last_spawned = do_refl;
+      if (!do_refl) break;
+      rd = reflect_dir(rd, nrm);                                            // !inside: n2 = n
+      ro = p;
+    }
+  }
+  // ---- phase 2: every shadow ray of the wave, dealt over all 64 lanes
+  const int lane = __lane_id();
+#ifdef RT_TILE_STATS
+  const uint64_t ts1 = wall_clock64();
+  int mx = nh, sm = nh;
+  for (int d = 32; d >= 1; d >>= 1) { mx = max(mx, __shfl_xor(mx, d)); sm += __shfl_xor(sm, d); }
+#endif
+  const int nl = S.n_lights;
+  const int hpr = nl > 0 ? (RT_SH_TRCAP / nl < 64 ? RT_SH_TRCAP / nl : 64) : 64;
+  for (int next = 0;;) {
+    const int pend = nh - next;
+    int incl = pend;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
+    }
+    const int total = __shfl(incl, 63);
+    if (total == 0) break;                                                  // wave-uniform
+    const int base = incl - pend;
+    const int take = base >= hpr ? 0 : (pend < hpr - base ? pend : hpr - base);
+    for (int i = 0; i < take; ++i) {
+      win->px[base + i] = hP[next + i][0];
+      win->py[base + i] = hP[next + i][1];
+      win->pz[base + i] = hP[next + i][2];
+    }
+    const int n_pub = total < hpr ? total : hpr;
+#ifdef RT_TILE_STATS
+    ++rounds;
+#endif
+    __syncthreads();
+    const int jobs = n_pub * nl;
+    for (int j = lane; j < jobs; j += 64) {                                 // :176-197
+      const int h = j % n_pub, k = j / n_pub;
+      const V3 p = {win->px[h], win->py[h], win->pz[h]};
+      const V3 lv = sub(ld3(S.lights[k].p), p);
+      win->tr[j] = shadow_transparency(S, p, normalized(lv), len(lv));
+    }
+    __syncthreads();
+    for (int i = 0; i < take; ++i) {                                        // L_h in light order
+      const int hh = next + i;
+      const V3 p = {hP[hh][0], hP[hh][1], hP[hh][2]};
+      const V3 nrm = {hN[hh][0], hN[hh][1], hN[hh][2]};
+      const Col c = {hC[hh][0], hC[hh][1], hC[hh][2]};
+      Col L = cmul(c, in_range(0.6, 0.6, 0.6));                             // ambient (:172)
+      for (int k = 0; k < nl; ++k) {                                        // :199-227
+        const double tr = win->tr[k * n_pub + base + i];
+        if (tr == 0.0) continue;
+        cptr<RtLight> lt = &S.lights[k];
+        const V3 sdir = normalized(sub(ld3(lt->p), p));
+        double ang = rt_acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
+        if (ang >= PI_D / 2.0) ang = PI_D - ang;
+        const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
+        const Col lc = intensify(intensify(Col{lt->col[0], lt->col[1], lt->col[2]}, inten), tr);
+        L = cadd(L, cmul(c, lc));
+      }
+      hC[hh][0] = L.r; hC[hh][1] = L.g; hC[hh][2] = L.b;
+    }
+    next += take;
+    __syncthreads();                                                        // the window is reused
+  }
+  // ---- phase 3: post-order combine, last hit first
+#ifdef RT_TILE_STATS
+  const uint64_t ts2 = wall_clock64();
+  if (stats_tile >= 0 && stats_tile < RT_STATS_TILES && lane == 0) {
+    g_tile_stats[stats_tile][0] = (uint32_t)(ts1 - ts0);
+    g_tile_stats[stats_tile][1] = (uint32_t)(ts2 - ts1);
+    g_tile_stats[stats_tile][2] = (uint32_t)mx | ((uint32_t)rounds << 8);
+    g_tile_stats[stats_tile][3] = (uint32_t)sm;
+  }
+#endif
+  Col C = {0.0, 0.0, 0.0};
+  for (int h = nh - 1; h >= 0; --h) {
+    const Col L = {hC[h][0], hC[h][1], hC[h][2]};
+    const double w = hW[h];
+    C = (h == nh - 1 && !last_spawned) ? L : cadd(intensify(L, 1.0 - w), intensify(C, w));   // :278-279
+  }
+  return C;
 }
 
 __device__ __forceinline__ DS make_ds(const RtDevScene& s) {
@@ -883,6 +1041,57 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   }
   if constexpr (CAL)
     if (threadIdx.x == 0) cost[tile] = (uint32_t)(wall_clock64() - t_start);   // vector store
+}
+
+// The deferred-shadow kernel for scenes without a transparent object (REFR = false), used for
+// launches of few tiles (a multi-GPU rank's share), whose time is set by their costliest tiles:
+// one wave per 8x8 tile as above, every tile on the deferred path (trace_deferred), and the
+// costliest tiles split over P = 2, 4 or 8 waves: wave `part` renders pixels
+// [part * 64/P, (part + 1) * 64/P) of the tile on its first 64/P lanes and its other lanes only
+// trace shadow rays (phase 2), so a costly tile's shadow work spreads over P x 64 lanes and its
+// latency -- the launch's tail -- shrinks.  Order entry: tile | part << 20 | log2(P) << 23 (built
+// by launch_bands after the calibration launch).  A kernel of its own: the megakernel path and
+// this one in ONE kernel measured 3.4x slower than either (profiles/r02g_ab.txt: both paths' code
+// hot on one CU at once).
+#ifndef RT_WAVES_PER_EU_DEFERRED
+#define RT_WAVES_PER_EU_DEFERRED 7
+#endif
+template <bool F64, bool CAL = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_DEFERRED))) void
+render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth,
+                            uint8_t* __restrict__ out, size_t stride, const int32_t* __restrict__ order,
+                            uint32_t* __restrict__ cost) {
+  __shared__ ShadowWin win;
+  const int lane = threadIdx.x & 63;
+  const uint32_t e = CAL || !order ? blockIdx.x : (uint32_t)order[blockIdx.x];
+  const unsigned tile = e & RT_SPLIT_TILE_MASK;
+  const int lp = (int)((e >> 23) & 3u), per = 64 >> lp;
+  const int pix = (int)((e >> 20) & 7u) * per + lane;
+  [[maybe_unused]] uint64_t t_start = 0;
+  if constexpr (CAL) t_start = wall_clock64();
+  const unsigned tiles_x = (unsigned)(S.width + 7) / 8;
+  const int x = (int)(tile % tiles_x) * 8 + (pix & 7);
+  const int r = (int)(tile / tiles_x) * 8 + (pix >> 3);
+  int y = 0;
+  bool valid = lane < per && x < S.width && r < n_rows;
+  if (valid) {
+    y = y_first + (r / band_rows) * band_pitch + r % band_rows;
+    valid = y < S.height;
+  }
+  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+  if (valid) camera_ray(S.cam, (double)x, (double)y, &ro, &rd);             // get_pixel(x as f64, y as f64)
+  const Col c = trace_deferred<RT_MAX_DEPTH_CAP + 1>(make_ds(S), ro, rd, max_depth, valid, &win, CAL ? (int)tile : -1);
+  if (valid) {
+    uint8_t* row = out + (size_t)r * stride;
+    if constexpr (F64) {
+      double* o = (double*)row + (size_t)x * 4;
+      o[0] = c.r; o[1] = c.g; o[2] = c.b; o[3] = 1.0;
+    } else {
+      ((uint32_t*)row)[x] = to_u8(c.r) | (to_u8(c.g) << 8) | (to_u8(c.b) << 16) | (255u << 24);
+    }
+  }
+  if constexpr (CAL)
+    if (lane == 0) cost[tile] = (uint32_t)(wall_clock64() - t_start);
 }
 
 template <bool REFR>
@@ -1217,6 +1426,7 @@ struct rt_ctx {
     int32_t* d_order = nullptr;
     uint32_t* d_cost = nullptr;
     size_t n_tiles = 0;
+    uint32_t grid = 0;                // entries of the order (> n_tiles when costly tiles are split)
     uint64_t last_use = 0;
     bool valid = false;               // set once the sorted order is on the device
   };
@@ -1243,6 +1453,31 @@ static bool tile_order_enabled() {
     return !(e && e[0] == '0');
   }();
   return on;
+}
+
+// Kernel choice for scenes without a transparent object: RT_DEFERRED=1 always takes the
+// deferred-shadow kernel, RT_DEFERRED=0 never (the per-lane megakernel, trace<false>); by default
+// launches of fewer than RT_DEFERRED_MAX_TILES tiles (~5 per wave slot of the chip) take it.
+// Same pixels either way.  Measured (profiles/r02g_inflight.txt, r02f_inflight.txt): a rank's
+// share of the 4K globes frame at N = 8 / 4 (16320 / 32640 tiles) takes 0.171 / 0.192 ms
+// deferred + split against 0.246 / 0.254 ms in the megakernel; at N = 2 / 1 (64800 / 129600
+// tiles) the megakernel is 15-20 % faster.
+#ifndef RT_DEFERRED_MAX_TILES
+#define RT_DEFERRED_MAX_TILES 40000
+#endif
+#ifndef RT_DEFERRED_DEFAULT
+#define RT_DEFERRED_DEFAULT (-1)
+#endif
+static bool deferred_mode(size_t n_tiles) {
+  static const int mode = [] {
+    const char* e = getenv("RT_DEFERRED");
+    return e ? (e[0] == '0' ? 0 : 1) : RT_DEFERRED_DEFAULT;
+  }();
+  static const size_t max_tiles = [] {
+    const char* e = getenv("RT_DEFERRED_MAX_TILES");
+    return e ? (size_t)atoll(e) : (size_t)RT_DEFERRED_MAX_TILES;
+  }();
+  return mode >= 0 ? mode == 1 : n_tiles < max_tiles;
 }
 
 static void drop_order(rt_ctx::OrderSlot& s) {
@@ -1296,6 +1531,16 @@ __attribute__((visibility("default"))) int rt_diag_cnt(unsigned long long* out32
   if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_rt_cnt), 32 * sizeof(unsigned long long)) != hipSuccess) return RT_ERR_DEVICE;
   static const unsigned long long zero[32] = {0};
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_rt_cnt), zero, sizeof(zero)) != hipSuccess) return RT_ERR_DEVICE;
+  return RT_OK;
+}
+#endif
+
+#ifdef RT_TILE_STATS
+// Diagnostic build only: the per-tile stats of the last calibration launch (4 words per tile).
+__attribute__((visibility("default"))) int rt_diag_tile_stats(uint32_t* out, size_t n_tiles) {
+  if (hipDeviceSynchronize() != hipSuccess) return RT_ERR_DEVICE;
+  if (n_tiles > RT_STATS_TILES) n_tiles = RT_STATS_TILES;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tile_stats), n_tiles * 16) != hipSuccess) return RT_ERR_DEVICE;
   return RT_OK;
 }
 #endif
@@ -1410,6 +1655,14 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   // Tile order: reuse the measured order for this exact geometry, else calibrate on this launch.
   const size_t n_tiles = (size_t)tiles_x * (size_t)tiles_y;
   const int32_t key[7] = {a0, a1, a2, a3, max_depth, f64 ? 1 : 0, c->dev.width};
+  const bool refr = c->dev.any_transparent != 0;
+  // Kernel choice for scenes without a transparent object (a function of the geometry only, so
+  // a geometry's tile order always belongs to one kernel): the per-lane megakernel is fastest when
+  // the launch fills the GPU many times over (throughput-bound); a launch of few tiles is bound by
+  // its costliest tiles' latency, which the deferred-shadow kernel with split costly tiles
+  // shortens (DESIGN.md "Deferred shadows").
+  const bool deferred = !refr && c->dev.n_lights <= RT_SH_TRCAP && RT_TILE_W == 8 && RT_TILE_H == 8 &&
+                        deferred_mode(n_tiles);
   rt_ctx::OrderSlot* slot = nullptr;
   bool calibrate = false;
   if (tile_order_enabled() && n_tiles >= RT_ORDER_MIN_TILES) {
@@ -1427,24 +1680,33 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
       RT_HIP(hipMemsetAsync(slot->d_cost, 0, n_tiles * sizeof(uint32_t), st));   // tiles that store no cost sort last
       memcpy(slot->key, key, sizeof(key));
       slot->n_tiles = n_tiles;
+      slot->grid = (uint32_t)n_tiles;
       calibrate = true;
     }
     slot->last_use = ++c->use_clock;
   }
   const int32_t* order = slot && !calibrate ? slot->d_order : nullptr;
   uint32_t* cost = calibrate ? slot->d_cost : nullptr;
+  if (order) grid.x = slot->grid;
   RT_HIP(hipEventRecord(c->ev0, st));
-  const bool refr = c->dev.any_transparent != 0;
 #define RT_LAUNCH_ROWS(R, F)                                                                                  \
   if (calibrate) hipLaunchKernelGGL((render_rows_kernel<R, F, true>), grid, block, 0, st, c->dev, a0, a1, a2, a3, \
                                     max_depth, target, tstride, order, cost);                                   \
   else hipLaunchKernelGGL((render_rows_kernel<R, F, false>), grid, block, 0, st, c->dev, a0, a1, a2, a3,         \
                           max_depth, target, tstride, order, cost);
+#define RT_LAUNCH_DEFERRED(F)                                                                                   \
+  if (calibrate) hipLaunchKernelGGL((render_rows_deferred_kernel<F, true>), grid, dim3(64), 0, st, c->dev, a0, a1, \
+                                    a2, a3, max_depth, target, tstride, order, cost);                            \
+  else hipLaunchKernelGGL((render_rows_deferred_kernel<F, false>), grid, dim3(64), 0, st, c->dev, a0, a1, a2, a3,  \
+                          max_depth, target, tstride, order, cost);
   if (refr && f64) { RT_LAUNCH_ROWS(true, true) }
   else if (refr) { RT_LAUNCH_ROWS(true, false) }
+  else if (deferred && f64) { RT_LAUNCH_DEFERRED(true) }
+  else if (deferred) { RT_LAUNCH_DEFERRED(false) }
   else if (f64) { RT_LAUNCH_ROWS(false, true) }
   else { RT_LAUNCH_ROWS(false, false) }
 #undef RT_LAUNCH_ROWS
+#undef RT_LAUNCH_DEFERRED
   RT_HIP(hipGetLastError());
   RT_HIP(hipEventRecord(c->ev1, st));
   c->timed = true;
@@ -1472,7 +1734,33 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     }
     if (getenv("RT_TILE_ORDER_IDENTITY"))   // diagnostic: the table without the reordering
       for (size_t i = 0; i < n_tiles; ++i) h_order[i] = (int32_t)i;
-    RT_HIP(hipMemcpyAsync(slot->d_order, h_order.data(), n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    if (deferred && n_tiles <= RT_SPLIT_TILE_MASK + 1) {
+      // Split the costliest tiles over P = 2, 4 or 8 waves (cost >= P * the median tile;
+      // RT_SPLIT_K overrides the factor 1, 0 disables): their shadow rays then spread over P x 64
+      // lanes.  Factor 1 / 1.5 / 2 / 3: N = 8 share 0.178 / 0.181 / 0.193 / 0.206 ms (r02f).
+      static const double split_k = [] { const char* e = getenv("RT_SPLIT_K"); return e ? atof(e) : 1.0; }();
+      std::vector<uint32_t> sorted_cost(h_cost);
+      std::nth_element(sorted_cost.begin(), sorted_cost.begin() + n_tiles / 2, sorted_cost.end());
+      const double med = std::max(1.0, (double)sorted_cost[n_tiles / 2]);
+      std::vector<int32_t> split;
+      split.reserve(n_tiles + n_tiles / 8);
+      for (size_t i = 0; i < n_tiles; ++i) {
+        const uint32_t t = (uint32_t)h_order[i];
+        int lp = 0;
+        while (split_k > 0.0 && lp < 3 && h_cost[t] >= split_k * med * (double)(2 << lp)) ++lp;
+        for (int part = 0; part < (1 << lp); ++part)
+          split.push_back((int32_t)(t | ((uint32_t)part << 20) | ((uint32_t)lp << 23)));
+      }
+      if (split.size() > n_tiles) {
+        int32_t* d = nullptr;
+        RT_HIP(hipMalloc((void**)&d, split.size() * sizeof(int32_t)));
+        (void)hipFree(slot->d_order);
+        slot->d_order = d;
+        h_order.swap(split);
+      }
+    }
+    slot->grid = (uint32_t)h_order.size();
+    RT_HIP(hipMemcpyAsync(slot->d_order, h_order.data(), h_order.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
     RT_HIP(hipStreamSynchronize(st));
     slot->valid = true;
     if (getenv("RT_TILE_ORDER_DEBUG")) {    // wave times in wall-clock ticks (100 MHz)
