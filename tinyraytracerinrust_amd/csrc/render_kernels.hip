@@ -1428,6 +1428,7 @@ struct rt_ctx {
     size_t n_tiles = 0;
     uint32_t grid = 0;                // entries of the order (> n_tiles when costly tiles are split)
     uint64_t last_use = 0;
+    bool deferred = false;            // ordered launches take the deferred-shadow kernel
     bool valid = false;               // set once the sorted order is on the device
   };
   static constexpr int RT_ORDER_SLOTS = 8;
@@ -1455,29 +1456,43 @@ static bool tile_order_enabled() {
   return on;
 }
 
-// Kernel choice for scenes without a transparent object: RT_DEFERRED=1 always takes the
-// deferred-shadow kernel, RT_DEFERRED=0 never (the per-lane megakernel, trace<false>); by default
-// launches of fewer than RT_DEFERRED_MAX_TILES tiles (~5 per wave slot of the chip) take it.
-// Same pixels either way.  Measured (profiles/r02g_inflight.txt, r02f_inflight.txt): a rank's
-// share of the 4K globes frame at N = 8 / 4 (16320 / 32640 tiles) takes 0.171 / 0.192 ms
-// deferred + split against 0.246 / 0.254 ms in the megakernel; at N = 2 / 1 (64800 / 129600
-// tiles) the megakernel is 15-20 % faster.
+// Kernel choice for scenes without a transparent object (REFR = false).  RT_DEFERRED=1 in the
+// environment always takes the deferred-shadow kernel, RT_DEFERRED=0 never (the per-lane
+// megakernel, trace<false>).  By default:
+//   * launches of fewer than RT_ORDER_MIN_TILES tiles (fewer tiles than the chip has wave slots:
+//     latency-bound by definition) take the deferred kernel;
+//   * larger launches calibrate on the megakernel; the ordered launches that follow take the
+//     deferred kernel with split tiles when the launch has fewer than RT_DEFERRED_MAX_TILES tiles
+//     AND its costliest tile is longer than RT_TAIL_RATIO x the work per wave slot (sum of tile
+//     costs / 7168): then the tail, not the throughput, sets the time.
+// Same pixels either way.  Measured (profiles/r02h_inflight.txt, r02j_*): a rank's share of the
+// 4K globes frame at N = 8 / 4 (16320 / 32640 tiles, tail ratio 3.5 / 1.8) takes 0.146-0.178 /
+// 0.187-0.204 ms deferred + split against 0.244 / 0.254 ms in the megakernel, 1080p globes d5
+// (ratio 1.7) 0.219 against 0.26-0.28 ms; at N = 2 / 1 (64800 / 129600 tiles, ratio 1.0 / 0.5),
+// and for the 1080p single sphere (32400 tiles, ratio 0.75: no tail to speak of), the megakernel
+// is 7-20 % faster.
 #ifndef RT_DEFERRED_MAX_TILES
 #define RT_DEFERRED_MAX_TILES 40000
+#endif
+#ifndef RT_TAIL_RATIO
+#define RT_TAIL_RATIO 1.0
 #endif
 #ifndef RT_DEFERRED_DEFAULT
 #define RT_DEFERRED_DEFAULT (-1)
 #endif
-static bool deferred_mode(size_t n_tiles) {
+static int deferred_mode() {
   static const int mode = [] {
     const char* e = getenv("RT_DEFERRED");
     return e ? (e[0] == '0' ? 0 : 1) : RT_DEFERRED_DEFAULT;
   }();
-  static const size_t max_tiles = [] {
+  return mode;
+}
+static size_t deferred_max_tiles() {
+  static const size_t v = [] {
     const char* e = getenv("RT_DEFERRED_MAX_TILES");
     return e ? (size_t)atoll(e) : (size_t)RT_DEFERRED_MAX_TILES;
   }();
-  return mode >= 0 ? mode == 1 : n_tiles < max_tiles;
+  return v;
 }
 
 static void drop_order(rt_ctx::OrderSlot& s) {
@@ -1656,13 +1671,12 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   const size_t n_tiles = (size_t)tiles_x * (size_t)tiles_y;
   const int32_t key[7] = {a0, a1, a2, a3, max_depth, f64 ? 1 : 0, c->dev.width};
   const bool refr = c->dev.any_transparent != 0;
-  // Kernel choice for scenes without a transparent object (a function of the geometry only, so
-  // a geometry's tile order always belongs to one kernel): the per-lane megakernel is fastest when
-  // the launch fills the GPU many times over (throughput-bound); a launch of few tiles is bound by
-  // its costliest tiles' latency, which the deferred-shadow kernel with split costly tiles
-  // shortens (DESIGN.md "Deferred shadows").
-  const bool deferred = !refr && c->dev.n_lights <= RT_SH_TRCAP && RT_TILE_W == 8 && RT_TILE_H == 8 &&
-                        deferred_mode(n_tiles);
+  // Kernel choice for scenes without a transparent object (see deferred_mode): the per-lane
+  // megakernel is fastest when the launch fills the GPU many times over (throughput-bound); a
+  // launch bound by its costliest tiles' latency takes the deferred-shadow kernel with split
+  // costly tiles (DESIGN.md "Deferred shadows").  An ordered launch takes its slot's choice.
+  const bool eligible = !refr && c->dev.n_lights <= RT_SH_TRCAP && RT_TILE_W == 8 && RT_TILE_H == 8;
+  const int dmode = deferred_mode();
   rt_ctx::OrderSlot* slot = nullptr;
   bool calibrate = false;
   if (tile_order_enabled() && n_tiles >= RT_ORDER_MIN_TILES) {
@@ -1688,6 +1702,12 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   const int32_t* order = slot && !calibrate ? slot->d_order : nullptr;
   uint32_t* cost = calibrate ? slot->d_cost : nullptr;
   if (order) grid.x = slot->grid;
+  bool deferred;
+  if (!eligible || dmode == 0) deferred = false;
+  else if (dmode == 1) deferred = true;
+  else if (order) deferred = slot->deferred;
+  else if (calibrate) deferred = false;                       // calibrate on the megakernel
+  else deferred = n_tiles < RT_ORDER_MIN_TILES || (!tile_order_enabled() && n_tiles < deferred_max_tiles());
   RT_HIP(hipEventRecord(c->ev0, st));
 #define RT_LAUNCH_ROWS(R, F)                                                                                  \
   if (calibrate) hipLaunchKernelGGL((render_rows_kernel<R, F, true>), grid, block, 0, st, c->dev, a0, a1, a2, a3, \
@@ -1734,7 +1754,15 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     }
     if (getenv("RT_TILE_ORDER_IDENTITY"))   // diagnostic: the table without the reordering
       for (size_t i = 0; i < n_tiles; ++i) h_order[i] = (int32_t)i;
-    if (deferred && n_tiles <= RT_SPLIT_TILE_MASK + 1) {
+    bool tail_bound = false;
+    if (eligible && dmode == -1 && n_tiles < deferred_max_tiles()) {
+      uint64_t sum = 0, mx = 0;
+      for (uint32_t v : h_cost) { sum += v; mx = v > mx ? v : mx; }
+      static const double ratio = [] { const char* e = getenv("RT_TAIL_RATIO"); return e ? atof(e) : RT_TAIL_RATIO; }();
+      tail_bound = (double)mx > ratio * (double)sum / 7168.0;
+    }
+    slot->deferred = eligible && (dmode == 1 || tail_bound);
+    if (slot->deferred && n_tiles <= RT_SPLIT_TILE_MASK + 1) {
       // Split the costliest tiles over P = 2, 4 or 8 waves (cost >= P * the median tile;
       // RT_SPLIT_K overrides the factor 1, 0 disables): their shadow rays then spread over P x 64
       // lanes.  Factor 1 / 1.5 / 2 / 3: N = 8 share 0.178 / 0.181 / 0.193 / 0.206 ms (r02f).
@@ -1768,8 +1796,9 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
       std::sort(v.begin(), v.end());
       double sum = 0.0;
       for (uint32_t x : v) sum += x;
-      fprintf(stderr, "tile order: %zu tiles, max %u, p99 %u, p90 %u, median %u, mean %.1f ticks\n", n_tiles, v.back(),
-              v[n_tiles * 99 / 100], v[n_tiles * 9 / 10], v[n_tiles / 2], sum / n_tiles);
+      fprintf(stderr, "tile order: %zu tiles, max %u, p99 %u, p90 %u, median %u, mean %.1f ticks; max / (sum / 7168) = %.3f; "
+              "ordered launches: %s kernel, %u entries\n", n_tiles, v.back(), v[n_tiles * 99 / 100], v[n_tiles * 9 / 10],
+              v[n_tiles / 2], sum / n_tiles, v.back() / (sum / 7168.0), slot->deferred ? "deferred" : "mega", slot->grid);
     }
   }
   if (!dev_out) {
