@@ -93,6 +93,10 @@ def parse():
     ap.add_argument("--streams", type=int, default=2,
                     help="anim120: frames dealt round-robin over this many HIP streams so independent "
                          "frames' kernels overlap (one 1080p frame does not fill the GPU to its end)")
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="before the warmup steps, render untimed frames for this long so the GPU reaches its "
+                         "sustained clocks (reported as `settle` in the line; 0 disables).  Measured: 20 steps after "
+                         "5 warmup steps alone run 0.675 ms/frame, 100 steps 0.603 (profiles/r02l_same_box.txt)")
     ap.add_argument("--png", default="", help="write the rendered frame (rank 0) to this PNG")
     ap.add_argument("--launcher-check", action="store_true",
                     help="CPU/gloo check of the N-rank launcher, band layout, all-gather and assembly with a "
@@ -298,6 +302,21 @@ def main():
         while pending:
             finish(pending.pop(0))
 
+    # settle (setup, untimed, not a step): the first launch of the geometry calibrates the tile
+    # order; then frames render until the GPU has run `settle_ms` at sustained clocks
+    settle_frames, ts = 0, time.perf_counter()
+    while settle_frames < 1 or (time.perf_counter() - ts) * 1e3 < a.settle_ms:
+        if multi:
+            rend.render_row_bands(y_first, band_rows, pitch, n_bands, slots[0], max_depth=depth, stream=stream)
+        else:
+            rend.render_rows(0, H, max_depth=depth, out=frames[0], stream=stream)
+        settle_frames += 1
+        if settle_frames % 8 == 0 or settle_frames == 1:
+            torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(dev)
+    settle = {"frames": settle_frames, "ms": round((time.perf_counter() - ts) * 1e3, 1)}
+    if multi:
+        dist.barrier()
     for i in range(a.warmup):
         step(i)
     drain()
@@ -404,6 +423,7 @@ def main():
         },
         "cpu_baseline": None,
         "frame_check": frame_check,
+        "settle": settle,
     }
     if multi:
         line["distributed"] = {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(),
@@ -519,6 +539,12 @@ def anim_main(a, json_out, rank, world, local, dev, multi):
             if evs is not None:
                 evs[j][1].record(stream)
 
+    settle_frames, ts = 0, time.perf_counter()          # untimed setup, as in main()
+    while settle_frames < 1 or (time.perf_counter() - ts) * 1e3 < a.settle_ms:
+        step()
+        torch.cuda.synchronize(dev)
+        settle_frames += len(rends)
+    settle = {"frames": settle_frames, "ms": round((time.perf_counter() - ts) * 1e3, 1)}
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -590,6 +616,7 @@ def anim_main(a, json_out, rank, world, local, dev, multi):
         },
         "rays": rays_line(fl, F * W * H * a.steps / elapsed),
         "host_compile_upload_ms_per_frame": round(prep_ms, 3),
+        "settle": settle,
         "cpu_baseline": None,
     }
     if world == 1 and not multi and not a.no_cpu_baseline:

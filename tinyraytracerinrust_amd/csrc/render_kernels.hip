@@ -1444,6 +1444,12 @@ using rt::fail;
     if (e_ != hipSuccess) return fail(RT_ERR_DEVICE, "%s failed: %s", #call, hipGetErrorString(e_)); \
   } while (0)
 
+#ifndef RT_ORDER_MODE_DEFAULT
+#define RT_ORDER_MODE_DEFAULT 0
+#endif
+#ifndef RT_ORDER_HEAVY_FRAC_DEFAULT
+#define RT_ORDER_HEAVY_FRAC_DEFAULT 0.1
+#endif
 #ifndef RT_ORDER_RUN
 #define RT_ORDER_RUN 1                // tiles per sorted run: 1 measured best (profiles/r01ah_tile_order_sweep.txt)
 #endif
@@ -1751,6 +1757,19 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     for (int32_t rr : run_order) {
       const int ty = rr / runs_x, tx0 = (rr % runs_x) * run;
       for (int tx = tx0; tx < tx0 + run && tx < tiles_x; ++tx) h_order[k++] = ty * tiles_x + tx;
+    }
+    // Order mode (RT_ORDER_MODE; experiments): 0 = longest first; 1 = zigzag (costliest,
+    // cheapest, 2nd costliest, 2nd cheapest, ...); 2 = the costliest RT_ORDER_HEAVY_FRAC of the
+    // tiles longest first, then the rest row-major (spatially coherent, mixed costs).
+    static const int order_mode = [] { const char* e = getenv("RT_ORDER_MODE"); return e ? atoi(e) : RT_ORDER_MODE_DEFAULT; }();
+    static const double heavy_frac = [] { const char* e = getenv("RT_ORDER_HEAVY_FRAC"); return e ? atof(e) : RT_ORDER_HEAVY_FRAC_DEFAULT; }();
+    if (order_mode == 1) {
+      std::vector<int32_t> z(n_tiles);
+      for (size_t i = 0, a = 0, b = n_tiles; i < n_tiles; ++i) z[i] = (i & 1) ? h_order[--b] : h_order[a++];
+      h_order.swap(z);
+    } else if (order_mode == 2) {
+      const size_t nh = std::min(n_tiles, (size_t)(heavy_frac * (double)n_tiles));
+      std::sort(h_order.begin() + nh, h_order.end());
     }
     if (getenv("RT_TILE_ORDER_IDENTITY"))   // diagnostic: the table without the reordering
       for (size_t i = 0; i < n_tiles; ++i) h_order[i] = (int32_t)i;

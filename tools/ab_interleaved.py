@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--size", default="3840x2160")
     ap.add_argument("--scene", default="globes")
     ap.add_argument("--time", type=float, default=0.0)
+    ap.add_argument("--burst", type=int, default=1,
+                    help="launches back to back per measurement (sustained clocks); the time per launch is "
+                         "the burst's wall time / burst")
     a = ap.parse_args()
     import torch
     W, H = (int(v) for v in a.size.split("x"))
@@ -38,16 +41,21 @@ def main():
         assert L.rt_ctx_create(0, ctypes.byref(cx)) == 0
         assert L.rt_ctx_upload(cx, sc) == 0
         ctxs.append((path, L, cx, []))
+    import time
     for rep in range(a.reps + 3):
         for path, L, cx, ms in ctxs:
-            rc = L.rt_render_rows(cx, 0, H, a.depth, ctypes.c_void_p(out.data_ptr()), ctypes.c_size_t(W * 4),
-                                  ctypes.c_void_p(st))
-            assert rc == 0, rc
             torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.burst):
+                rc = L.rt_render_rows(cx, 0, H, a.depth, ctypes.c_void_p(out.data_ptr()), ctypes.c_size_t(W * 4),
+                                      ctypes.c_void_p(st))
+                assert rc == 0, rc
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) * 1e3 / a.burst
             v = ctypes.c_float()
             L.rt_ctx_last_kernel_ms(cx, ctypes.byref(v))
             if rep >= 3:
-                ms.append(v.value)
+                ms.append(v.value if a.burst == 1 else dt)
     base = None
     for path, L, cx, ms in ctxs:
         med = statistics.median(ms)

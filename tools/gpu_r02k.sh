@@ -1,0 +1,8 @@
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out
+L=tinyraytracerinrust_amd
+B=$L/build
+timeout -k 10 300 python tools/ab_interleaved.py $L/librt_mi355x.so $B/librt_mi355x_zig.so $B/librt_mi355x_hf05.so $B/librt_mi355x_hf15.so $B/librt_mi355x_hf30.so --reps 8 --burst 10 > $O/r02k_order_ab.txt 2>&1 || { tail $O/r02k_order_ab.txt; exit 1; }
+timeout -k 10 300 python tools/ab_interleaved.py $L/librt_mi355x.so $B/librt_mi355x_zig.so $B/librt_mi355x_hf05.so $B/librt_mi355x_hf15.so $B/librt_mi355x_hf30.so --reps 8 --burst 10 --size 1920x1080 --depth 5 >> $O/r02k_order_ab.txt 2>&1 || { tail $O/r02k_order_ab.txt; exit 1; }
+cat $O/r02k_order_ab.txt
