@@ -619,15 +619,16 @@ struct BufRec {
 
 // Frame-stack slots in LDS.  The first KL frames of every lane's stack (A.r, A.g, A.b, w) live in
 // LDS laid out [frame][component][lane], so each access is one conflict-free ds_*_b64; deeper
-// frames (chains longer than KL, rare) use the private array, i.e. scratch.  8 KB per wave for
-// KL = 4: 16 one-wave workgroups per CU (4 waves/SIMD) take 128 of the 160 KB.  Measured on
-// MI355X (profiles/r01r_lds_stack_ab.txt): KL = 4 is 0.2-0.8 % SLOWER than the scratch stack at
-// 4K globes d=10 (the pushes are fire-and-forget and the pops few), so the product keeps KL = 0;
-// -DRT_LDS_FRAMES=4 builds the variant.
+// frames (chains longer than KL, rare) use the private array, i.e. scratch.  KL = 2: 4 KB per
+// one-wave workgroup, 80 of the 160 KB at 5 waves/SIMD.  With the megakernel at 5 waves/SIMD
+// (below) the stack was the last large source of scratch traffic: KL = 2 cuts the 4K globes
+// launch's HBM traffic from 0.245 to 0.105 GB (writes 0.21 -> 0.082 GB, 2.5x the 33 MB frame) at
+// equal time (+0.4 %, noise; KL = 4: 0.089 GB but 5 % slower), profiles/r02t_*.  (At 7 waves/SIMD,
+// round 1, KL = 4 measured 0.2-0.8 % slower than the scratch stack, profiles/r01r_lds_stack_ab.txt.)
 #define LDS_AS __attribute__((address_space(3)))
 typedef LDS_AS double lds_f64;
 #ifndef RT_LDS_FRAMES
-#define RT_LDS_FRAMES 0
+#define RT_LDS_FRAMES 2
 #endif
 
 // get_ray_color (raytracer.rs:132-287) for one primary ray, recursion unrolled onto a per-lane
@@ -978,15 +979,17 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
 // (a contiguous tile [y0, y1) is one band; the cyclic multi-GPU layout deals bands of
 // band_rows rows with pitch world * band_rows).  Workgroup = 16x16 output pixels, wave = 8x8.
 // Waves per SIMD (VGPR budget 512 / N) per instantiation: reflection-only scenes (REFR = false)
-// run 7 (<= 72 VGPRs; with RT_LIGHT_GROUP 1: 7.4 % faster than 5 waves on 4K globes, 8 waves
-// spills and is 23 % slower), refraction scenes keep 4 (128 VGPRs: their deeper frame state
-// spills at 5, 1.6-3.5 % slower on spinning_globes), profiles/r01ac_ab_sched.txt,
-// profiles/r01ad_ab_light_group.txt.
+// run 5 (<= 102 VGPRs, 96 used, 6 spilled).  Round 1 chose 7 (72 VGPRs, ~58 spilled) from A/B
+// runs that synchronised after every launch; with launches back to back (sustained clocks,
+// tools/ab_interleaved.py --burst) 5 is 1-3 % faster than 7 and cuts the launch's HBM traffic 9x
+// (2.30 -> 0.245 GB: the spills went to scratch), 6 is 5 % slower, 8 spills and is 1.7x slower
+// (profiles/r02o_waves_sustained.txt, r02q_ab.txt, r02r_ab.txt).  Refraction scenes keep 4
+// (128 VGPRs; 3 is equal, 5 is 1.5 % slower, profiles/r02s_ab.txt).
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 4
 #endif
 #ifndef RT_WAVES_PER_EU_NOREFR
-#define RT_WAVES_PER_EU_NOREFR 7
+#define RT_WAVES_PER_EU_NOREFR 5
 #endif
 #define RT_WAVES(REFR) ((REFR) ? RT_WAVES_PER_EU : RT_WAVES_PER_EU_NOREFR)
 // Workgroup = RT_WG_WX x RT_WG_WY waves of 8x8 pixels.
