@@ -262,6 +262,12 @@ def main():
     if multi and not overlap:
         K = 1
     nbuf = K + 1 if multi else K     # N = 1: buffer b is only ever written on stream b
+    # With several frames in flight the launches overlap, so no launch's tail leaves the GPU idle:
+    # the per-lane megakernel then beats the deferred-shadow kernel that the library picks for a
+    # lone tail-bound launch (a rank's share at N = 4 / 8 with K = 4: 0.148 / 0.076 ms against
+    # 0.182 / 0.093 ms, profiles/r02x_inflight_*.txt).
+    if K >= 3:
+        rend.set_kernel("mega")
     rstreams = [stream] if K == 1 else [torch.cuda.Stream(dev) for _ in range(K)]
     slots = [torch.zeros((slot_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
     gath = [torch.zeros((world * slot_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
@@ -394,6 +400,7 @@ def main():
             "collective": None if not multi else "all_gather_into_tensor (RCCL)" + (
                 ", overlapped with later frames" if overlap else ""),
             "frames_in_flight": K,
+            "kernel": "megakernel (rt_ctx_set_option)" if K >= 3 else "library's choice (auto)",
             "frame_bytes": W * H * 4,
         },
         "rays": rays_line(fl, W * H * a.steps / elapsed),
@@ -428,7 +435,8 @@ def main():
     if multi:
         line["distributed"] = {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(),
                                "rows_per_rank": rows_per_rank, "layout": layout, "band_rows": band,
-                               "frames_in_flight": K, "frame_check": frame_check}
+                               "frames_in_flight": K,
+            "kernel": "megakernel (rt_ctx_set_option)" if K >= 3 else "library's choice (auto)", "frame_check": frame_check}
     if world == 1 and not multi and not a.no_cpu_baseline:
         cb = cpu_baseline(text, W, H, t, depth, a.cpu_threads)
         cb["gpu_over_cpu"] = round(line["value"] / cb["value"], 1)

@@ -216,6 +216,19 @@ int rt_antialias(rt_ctx* ctx, const uint8_t* src_rgba8, size_t src_stride, doubl
  * stream around the kernel). */
 int rt_ctx_last_kernel_ms(rt_ctx* ctx, float* ms);
 int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launch */
+/* Tuning options of a context.  No option changes a single pixel; they only choose how the
+ * kernels run.  RT_OPT_KERNEL selects the render kernel for scenes without a transparent object:
+ *   RT_KERNEL_AUTO (default): a launch bound by its costliest tiles (fewer tiles than ~5 per wave
+ *     slot, costliest tile > the work per slot) takes the deferred-shadow kernel with the costly
+ *     tiles split over several waves, every other launch the per-lane megakernel;
+ *   RT_KERNEL_MEGA: always the megakernel -- best when several frames are in flight on different
+ *     streams (their launches overlap, so no launch's tail leaves the GPU idle);
+ *   RT_KERNEL_DEFERRED: always the deferred-shadow kernel.
+ * Changing the kernel drops the context's tile orders (the next launch of each geometry
+ * calibrates again).  Scenes with a transparent object always take the refraction megakernel. */
+typedef enum rt_option { RT_OPT_KERNEL = 0 } rt_option;
+typedef enum rt_kernel_choice { RT_KERNEL_AUTO = 0, RT_KERNEL_MEGA = 1, RT_KERNEL_DEFERRED = 2 } rt_kernel_choice;
+int rt_ctx_set_option(rt_ctx* ctx, int32_t option, int32_t value);
 void rt_ctx_free(rt_ctx* ctx);
 
 /* ---- output ----------------------------------------------------------------------------- */

@@ -19,6 +19,8 @@ STATUS_NAMES = {
     -5: "RT_ERR_DEVICE", -6: "RT_ERR_UNSUPPORTED", -7: "RT_ERR_NOMEM",
 }
 RT_CSG_UNION, RT_CSG_INTERSECTION, RT_CSG_DIFFERENCE = 0, 1, 2
+RT_OPT_KERNEL = 0
+RT_KERNEL_AUTO, RT_KERNEL_MEGA, RT_KERNEL_DEFERRED = 0, 1, 2
 
 
 class RtError(RuntimeError):
@@ -92,6 +94,7 @@ SIGNATURES = {
                           ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64), _P]),
     "rt_ctx_last_kernel_ms": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
     "rt_ctx_synchronize": (_I, [_P]),
+    "rt_ctx_set_option": (_I, [_P, ctypes.c_int32, ctypes.c_int32]),
     "rt_ctx_free": (None, [_P]),
     "rt_write_png": (_I, [ctypes.c_char_p, _P, _U32, _U32, ctypes.c_size_t, _I]),
     "rt_read_png_rgba8": (_I, [ctypes.c_char_p, ctypes.POINTER(_P), ctypes.POINTER(_U32),

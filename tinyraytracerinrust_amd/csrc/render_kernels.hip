@@ -1412,6 +1412,7 @@ struct rt_ctx {
   size_t blob_bytes = 0;
   RtDevScene dev;
   int32_t max_depth = 10;
+  int32_t kernel_opt = RT_KERNEL_AUTO;  // rt_ctx_set_option(RT_OPT_KERNEL)
   bool uploaded = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -1685,7 +1686,8 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   // launch bound by its costliest tiles' latency takes the deferred-shadow kernel with split
   // costly tiles (DESIGN.md "Deferred shadows").  An ordered launch takes its slot's choice.
   const bool eligible = !refr && c->dev.n_lights <= RT_SH_TRCAP && RT_TILE_W == 8 && RT_TILE_H == 8;
-  const int dmode = deferred_mode();
+  // -1 auto, 0 megakernel, 1 deferred: the context's option, else the environment's default
+  const int dmode = c->kernel_opt == RT_KERNEL_MEGA ? 0 : c->kernel_opt == RT_KERNEL_DEFERRED ? 1 : deferred_mode();
   rt_ctx::OrderSlot* slot = nullptr;
   bool calibrate = false;
   if (tile_order_enabled() && n_tiles >= RT_ORDER_MIN_TILES) {
@@ -2099,6 +2101,20 @@ int rt_ctx_last_kernel_ms(rt_ctx* c, float* ms) {
   if (!c->timed) return fail(RT_ERR_INVALID, "no launch recorded");
   RT_HIP(hipEventSynchronize(c->ev1));
   RT_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return RT_OK;
+}
+
+int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
+  if (!c) return fail(RT_ERR_INVALID, "null context");
+  if (option != RT_OPT_KERNEL) return fail(RT_ERR_INVALID, "unknown option %d", option);
+  if (value != RT_KERNEL_AUTO && value != RT_KERNEL_MEGA && value != RT_KERNEL_DEFERRED)
+    return fail(RT_ERR_INVALID, "RT_OPT_KERNEL value %d", value);
+  if (value != c->kernel_opt) {
+    // tile orders were built for one kernel (split entries only for the deferred one): rebuild
+    RT_HIP(hipSetDevice(c->device));
+    drop_orders(c);
+    c->kernel_opt = value;
+  }
   return RT_OK;
 }
 

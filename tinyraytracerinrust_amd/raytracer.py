@@ -274,6 +274,11 @@ class Renderer:
                                     None))
         return out
 
+    def set_kernel(self, kernel: str = "auto") -> None:
+        """rt_ctx_set_option(RT_OPT_KERNEL): "auto", "mega" or "deferred" (same pixels; see rt_abi.h)."""
+        v = {"auto": _lib.RT_KERNEL_AUTO, "mega": _lib.RT_KERNEL_MEGA, "deferred": _lib.RT_KERNEL_DEFERRED}[kernel]
+        check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_KERNEL, v))
+
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()
         check(lib().rt_ctx_last_kernel_ms(self.h, ctypes.byref(ms)))
