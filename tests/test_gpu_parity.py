@@ -79,6 +79,11 @@ EDGE_SCENES = {
     "huge_wall": "draw(sphere(<0, 0, 2000000>, 1999000, red * 0.8, 0.3))\n"
                  "draw(sphere(<0, 0, 0>, 20, red, 0.5))\ndraw(cube(<25, -10, 0>, 10, red * 0.5, 0.2))",
     # translation-only inverses with -0 entries: the diagonal-affine transform short form
+    # materials outside [0, 1] (negative colour, reflectivity > 1, transparency > 1): the kernels
+    # must keep the compare/select clamps here (RtDevScene::colour_fast = 0)
+    "odd_materials": "draw(sphere(<0, 0, 0>, 25, red * (0 - 0.5), 1.3))\n"   # (-0.5, -0, -0), refl 1.3
+                     "draw(plane(<0, 1, 0>, 20, rgb(0.3, 0.3, 0.9), 0.5))\n"
+                     "draw(sphere(<30, 0, -10>, 12, rgb(0.8, 0.8, 0.1), 0.2, 1.2))",
     "signed_zero_xf": "translate(0, 5, 0) draw(sphere(<0, 0, 0>, 30, red, 0.3))\n"
                       "translate(0, -30, 0) draw(cube(<0, 0, 0>, 20, red * 0.5, 0.5))\n"
                       "scale(1, 0.5, 1) draw(sphere(<30, 0, 0>, 10, red * 0.2, 0.4, 0.5))",

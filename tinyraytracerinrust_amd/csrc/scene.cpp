@@ -449,6 +449,15 @@ int flatten(const rt_scene& s, FlatScene* out) {
   f.max_depth = s.max_depth;
   f.any_transparent = 0;
   f.shadow_early_out = 1;
+  // colour_fast: every operand of every colour op (color.rs:36-90) is finite and >= +0 (no NaN,
+  // no -0, nothing negative), so the kernels' clamps may take the min/max form (render_kernels.hip
+  // in_limit<FC>).  Sufficient: every solid material colour and light colour channel finite with
+  // a clear sign bit, every reflectivity and transparency finite, sign bit clear, <= 1.  Then the
+  // ambient term, the Lambert intensities (in [0, 1], 0 for NaN angles), the shadow products, the
+  // weights 1 - w and w of every fold, and every clamped colour are all finite and >= +0.
+  f.colour_fast = 1;
+  auto nonneg = [](double x) { return std::isfinite(x) && !std::signbit(x); };
+  auto unit = [&](double x) { return nonneg(x) && x <= 1.0; };
   for (const ObjectRec& o : s.objects) {
     Flattener fl{s, f};
     fl.node_begin = (int32_t)f.nodes.size();
@@ -510,12 +519,15 @@ int flatten(const rt_scene& s, FlatScene* out) {
     ob.shadow_skip = m.transparency == 1.0;
     if (m.transparency != 0.0) f.any_transparent = 1;
     if (!isfinite(m.transparency)) f.shadow_early_out = 0;
+    if (!unit(m.reflectivity) || !unit(m.transparency)) f.colour_fast = 0;
+    if (m.texture < 0 && !(nonneg(m.color[0]) && nonneg(m.color[1]) && nonneg(m.color[2]))) f.colour_fast = 0;
     f.objects.push_back(ob);
   }
   build_hierarchy(&f);
   for (const LightRec& l : s.lights) {
     RtLight L;
     for (int i = 0; i < 3; ++i) { L.p[i] = l.p[i]; L.col[i] = l.color[i]; }
+    if (!(nonneg(l.color[0]) && nonneg(l.color[1]) && nonneg(l.color[2]))) f.colour_fast = 0;
     f.lights.push_back(L);
   }
   int64_t off = 0;

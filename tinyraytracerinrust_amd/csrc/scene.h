@@ -50,6 +50,7 @@ struct FlatScene {
   RtCamera cam;
   int32_t width, height, max_depth;
   int32_t any_transparent, shadow_early_out;
+  int32_t colour_fast;   // every colour-op operand is finite and >= +0 (see flatten)
 };
 
 // Transformation math (transformation.rs:104-220), exact f64 op order.
