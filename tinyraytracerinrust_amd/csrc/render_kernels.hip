@@ -1290,8 +1290,8 @@ __global__ __launch_bounds__(256) void aa_expand_kernel(AaGrid G, uint32_t n, in
   for (int w = 0; w < RT_AA_HAVE_WORDS; ++w) h[w] = have[w];
 }
 
-template <bool REFR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU))) void aa_trace_kernel(
+template <bool REFR, bool FC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES(REFR)))) void aa_trace_kernel(
     RtDevScene S, AaGrid G, const uint32_t* __restrict__ edges, const uint2* __restrict__ req, uint32_t n, int max_depth) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1300,7 +1300,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
   const int sx = r.y & 0xff, sy = r.y >> 8, sz = G.size;
   V3 ro, rd;
   camera_ray(S.cam, (double)x + ((double)sx / (double)sz), (double)y + ((double)sy / (double)sz), &ro, &rd);   // :108-112
-  const Col c = trace<REFR>(make_ds(S), ro, rd, max_depth);
+  const Col c = trace<REFR, NoRec, 0, FC>(make_ds(S), ro, rd, max_depth);
   G.col[(size_t)r.x * sz * sz + sx * sz + sy] = {c.r, c.g, c.b, 1.0};
 }
 
@@ -1993,8 +1993,13 @@ int rt_antialias(rt_ctx* c, const uint8_t* src_rgba8, size_t src_stride, double 
       if (n_req == 0) break;
       rays += n_req;
       const dim3 rg((n_req + 255) / 256);
-      if (c->dev.any_transparent) hipLaunchKernelGGL((aa_trace_kernel<true>), rg, blk, 0, st, c->dev, G, edges, req, n_req, (int)max_depth);
-      else hipLaunchKernelGGL((aa_trace_kernel<false>), rg, blk, 0, st, c->dev, G, edges, req, n_req, (int)max_depth);
+      const bool fc = c->dev.colour_fast != 0 && fast_clamp_enabled();
+#define RT_LAUNCH_AA(R, F) hipLaunchKernelGGL((aa_trace_kernel<R, F>), rg, blk, 0, st, c->dev, G, edges, req, n_req, (int)max_depth)
+      if (c->dev.any_transparent && fc) RT_LAUNCH_AA(true, true);
+      else if (c->dev.any_transparent) RT_LAUNCH_AA(true, false);
+      else if (fc) RT_LAUNCH_AA(false, true);
+      else RT_LAUNCH_AA(false, false);
+#undef RT_LAUNCH_AA
     }
     if (err == RT_OK) {
       hipLaunchKernelGGL(aa_resolve_kernel, eg, blk, 0, st, G, edges, n_edges, (int)level, threshold, u8, u8s, f64, f64s);
