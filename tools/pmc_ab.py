@@ -1,6 +1,6 @@
 """Summarise rocprofv3 --pmc passes of several variants (diagnostic): for each
 gpurun_out/<tag>_<variant>_pmc_*/run_counter_collection.csv, the mean of every counter over the
-product dispatches of the render kernels (the calibration instantiation, last template argument
+product dispatches of the render kernels (the calibration instantiation, template argument CAL =
 `true`, excluded), per kernel name.  usage: python tools/pmc_ab.py TAG [OUT.json]"""
 import csv
 import glob
@@ -21,8 +21,12 @@ def main(tag, out=None):
             for r in csv.DictReader(open(f)):
                 name = r["Kernel_Name"]
                 m = re.search(r"(render_rows\w*kernel)<([^>]*)>", name)
-                if not m or m.group(2).split(",")[-1].strip() == "true":
+                if not m:
                     continue
+                targs = [t.strip() for t in m.group(2).split(",")]
+                cal_pos = 1 if "deferred" in m.group(1) else 2      # <REFR, F64, CAL, FC> / <F64, CAL, FC>
+                if len(targs) > cal_pos and targs[cal_pos] == "true":
+                    continue                                        # the calibration instantiation
                 key = f"{m.group(1)}<{m.group(2)}>"
                 res.setdefault(variant, {}).setdefault(key, defaultdict(list))[r["Counter_Name"]].append(
                     float(r["Counter_Value"]))

@@ -29,10 +29,10 @@ def main(tag="r01", config="globes4k", kernel="render_rows_kernel"):
     agg = defaultdict(list)
     for f in glob.glob(os.path.join(out, f"{tag}_pmc_*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            # the product instantiation only: render_rows_kernel<REFR, F64, CAL=false>; the one
+            # the product instantiation only: render_rows_kernel<REFR, F64, CAL=false, FC>; the one
             # calibration launch per geometry (CAL=true, "...ELb1EEEv") is excluded
             m = re.search(r"render_rows_kernel<([^>]*)>", r["Kernel_Name"])
-            cal = m is not None and len(m.group(1).split(",")) == 3 and m.group(1).split(",")[2].strip() == "true"
+            cal = m is not None and len(m.group(1).split(",")) >= 3 and m.group(1).split(",")[2].strip() == "true"
             if kernel in r["Kernel_Name"] and not cal:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     mean = {k: sum(v) / len(v) for k, v in agg.items()}
