@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--layout", default="cyclic", choices=["contiguous", "cyclic"],
                     help="row tiling for N > 1 (cyclic 8-row bands balance sky vs floor rows)")
     ap.add_argument("--band", type=int, default=8)
+    ap.add_argument("--gather", default="rgb", choices=["rgb", "rgba"],
+                    help="N > 1: ranks render their bands as packed RGB8 and the all-gather moves 3 bytes per "
+                         "pixel (the assembly writes the RGBA8 frame, A = 255); rgba gathers RGBA8 rows")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1: do not overlap frame k's all-gather with frame k+1's render")
     ap.add_argument("--force-collective", action="store_true",
@@ -269,8 +272,9 @@ def main():
     if K >= 3:
         rend.set_kernel("mega")
     rstreams = [stream] if K == 1 else [torch.cuda.Stream(dev) for _ in range(K)]
-    slots = [torch.zeros((slot_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
-    gath = [torch.zeros((world * slot_rows, W, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
+    ch = 3 if a.gather == "rgb" else 4
+    slots = [torch.zeros((slot_rows, W, ch), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
+    gath = [torch.zeros((world * slot_rows, W, ch), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
     frames = [frame] + [torch.zeros_like(frame) for _ in range(nbuf - 1)]
     free_ev = [None] * nbuf    # buffer b's last gather and assembly are done once this event fires
     pending = []               # (work, buffer, stream) of gathers not yet assembled, oldest first
@@ -397,7 +401,7 @@ def main():
                         + f" {W}x{H} t={t:g} max_depth {depth}, one frame per step",
             "scene": f"{scene}.scene" if scene == "globes" else SPHERE_SCENE, "width": W, "height": H, "time": t, "max_depth": depth,
             "parallelism": f"rowtile{world}" + ("" if not multi else f"-{layout}" + (f"{band}" if layout == "cyclic" else "")),
-            "collective": None if not multi else "all_gather_into_tensor (RCCL)" + (
+            "collective": None if not multi else f"all_gather_into_tensor (RCCL) of {a.gather.upper()}8 band slots" + (
                 ", overlapped with later frames" if overlap else ""),
             "frames_in_flight": K,
             "kernel": "megakernel (rt_ctx_set_option)" if K >= 3 else "library's choice (auto)",
@@ -477,21 +481,25 @@ def launcher_check(a, json_out):
     layout = a.layout
     band = a.band if layout == "cyclic" else -(-H // world)
 
-    def pattern(ys):
+    ch = 3 if a.gather == "rgb" else 4
+
+    def pattern(ys, channels=4):
         ys = torch.as_tensor(ys, dtype=torch.int64).view(-1, 1).expand(-1, W)
         xs = torch.arange(W, dtype=torch.int64).view(1, -1).expand(len(ys), -1)
-        return torch.stack([ys & 255, ys >> 8, xs & 255, xs >> 8], -1).to(torch.uint8)
+        a_ = torch.full_like(xs, 255) if channels == 4 and ch == 3 else xs >> 8    # RGB slots: assembled A = 255
+        px = torch.stack([ys & 255, ys >> 8, xs & 255, a_], -1).to(torch.uint8)
+        return px[..., :channels]
 
     slot_rows = D.rows_per_rank(H, world, layout, band)
     y_first, band_rows, pitch, n_bands = D.band_params(H, world, rank, layout, band)
-    slot = torch.zeros((slot_rows, W, 4), dtype=torch.uint8)
+    slot = torch.zeros((slot_rows, W, ch), dtype=torch.uint8)
     ys = [y_first + (r // band_rows) * pitch + r % band_rows for r in range(band_rows * n_bands)] if band_rows else []
     keep = [r for r, y in enumerate(ys) if y < H]
     if keep:
-        slot[keep] = pattern([ys[r] for r in keep])
+        slot[keep] = pattern([ys[r] for r in keep], ch)
     ok = True
     for _ in range(max(1, a.steps)):
-        gath = torch.empty((world * slot_rows, W, 4), dtype=torch.uint8)
+        gath = torch.empty((world * slot_rows, W, ch), dtype=torch.uint8)
         dist.all_gather_into_tensor(gath, slot)
         frame = D.assemble(gath, H, world, layout, band)
         ok = ok and torch.equal(frame, pattern(range(H)))
@@ -502,7 +510,7 @@ def launcher_check(a, json_out):
                 "n_gpus": world, "steps": a.steps, "warmup": 0,
                 "distributed": {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(),
                                 "rows_per_rank": [n for _, n in flags], "layout": layout, "band_rows": band,
-                                "frame_check": all(f for f, _ in flags)},
+                                "gather": a.gather, "frame_check": all(f for f, _ in flags)},
                 "config": {"width": W, "height": H}}
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()

@@ -174,6 +174,17 @@ int rt_render_row_bands(rt_ctx* ctx, uint32_t y_first, uint32_t band_rows, uint3
 int rt_assemble_row_bands(const uint8_t* gathered, size_t gathered_stride, uint32_t world, uint32_t slot_rows,
                           uint32_t band_rows, uint32_t height, size_t row_bytes, uint8_t* frame,
                           size_t frame_stride, void* stream);
+/* The band layout above written as packed RGB8 (3 bytes per pixel, R,G,B; alpha is always 255):
+ * the multi-GPU all-gather then moves 3/4 of the bytes.  row_stride_bytes >= 3 * width. */
+int rt_render_row_bands_rgb8(rt_ctx* ctx, uint32_t y_first, uint32_t band_rows, uint32_t band_pitch,
+                             uint32_t n_bands, int32_t max_depth, uint8_t* rgb8, size_t row_stride_bytes,
+                             void* stream);
+/* rt_assemble_row_bands from gathered packed RGB8 slot rows (rt_render_row_bands_rgb8) into RGBA8
+ * frame rows (A = 255, the bytes rt_render_rows writes): `width` pixels per row; frame rows 4-byte
+ * aligned.  Device pointers only, one launch on `stream`, asynchronous. */
+int rt_assemble_row_bands_rgb8(const uint8_t* gathered, size_t gathered_stride, uint32_t world, uint32_t slot_rows,
+                               uint32_t band_rows, uint32_t height, uint32_t width, uint8_t* frame,
+                               size_t frame_stride, void* stream);
 /* Same as rt_render_rows, pre-quantisation colours: 4 doubles per pixel (r,g,b,a) -- the
  * `Vec<Color>` rows. */
 int rt_render_rows_f64(rt_ctx* ctx, uint32_t y0, uint32_t y1, int32_t max_depth,

@@ -25,12 +25,13 @@ def _run(*args):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("world,layout", [(2, "cyclic"), (2, "contiguous"), (3, "cyclic")])
-def test_self_launch_gloo(world, layout):
-    line = _run("--gpus", str(world), "--launcher-check", "--layout", layout, "--steps", "2")
+@pytest.mark.parametrize("world,layout,gather", [(2, "cyclic", "rgb"), (2, "contiguous", "rgb"), (3, "cyclic", "rgb"),
+                                                 (2, "cyclic", "rgba")])
+def test_self_launch_gloo(world, layout, gather):
+    line = _run("--gpus", str(world), "--launcher-check", "--layout", layout, "--steps", "2", "--gather", gather)
     d = line["distributed"]
     assert line["n_gpus"] == world
-    assert d["world_size_seen"] == world and d["backend"] == "gloo"
+    assert d["world_size_seen"] == world and d["backend"] == "gloo" and d["gather"] == gather
     assert d["frame_check"] is True
     assert len(d["rows_per_rank"]) == world and sum(d["rows_per_rank"]) == line["config"]["height"]
 

@@ -75,8 +75,8 @@ def globes4k_oracle(worldmap):
     return oracle_frame(scene_text("globes"), 0.0, 3840, 2160, 10)
 
 
-@pytest.mark.parametrize("world", [8, 4, 2])
-def test_globes4k_rank_bands_full_frame(T, globes4k_oracle, world):
+@pytest.mark.parametrize("world,channels", [(8, 3), (4, 4), (2, 3)])
+def test_globes4k_rank_bands_full_frame(T, globes4k_oracle, world, channels):
     """BASELINE config 4 as the multi-GPU path renders it: every rank's cyclic 8-row bands
     (rt_render_row_bands: the calibration launch, then the ordered launch -- at N = 8 the
     deferred-shadow kernel with the costliest tiles split over several waves, at N <= 4 the
@@ -90,7 +90,7 @@ def test_globes4k_rank_bands_full_frame(T, globes4k_oracle, world):
     slot_rows = D.rows_per_rank(H, world, "cyclic", 8)
     frames = []
     for launch in range(2):
-        gath = torch.zeros((world * slot_rows, W, 4), dtype=torch.uint8, device="cuda")
+        gath = torch.zeros((world * slot_rows, W, channels), dtype=torch.uint8, device="cuda")   # 3: packed RGB8 slots
         for rank in range(world):
             y_first, band_rows, pitch, n_bands = D.band_params(H, world, rank, "cyclic", 8)
             r.render_row_bands(y_first, band_rows, pitch, n_bands, gath[rank * slot_rows:(rank + 1) * slot_rows])

@@ -280,3 +280,39 @@ def test_tile_orders_of_interleaved_geometries_on_two_streams(T):
     torch.cuda.synchronize()
     for g, o in outs:
         assert np.array_equal(o.cpu().numpy(), want[g]), f"geometry {g}"
+
+
+@pytest.mark.parametrize("world,layout,band", [(3, "cyclic", 8), (8, "contiguous", 0), (5, "cyclic", 16)])
+def test_rgb8_row_bands_assemble_like_ranks(T, world, layout, band):
+    """The multi-GPU path with packed RGB8 slots (rt_render_row_bands_rgb8, the all-gather moves 3
+    bytes per pixel) assembled into RGBA8 (rt_assemble_row_bands_rgb8): equals the plain frame."""
+    import torch
+    from tinyraytracerinrust_amd import distributed as D
+    W, H = 203, 150                                  # odd width: the RGB rows are not 4-byte multiples
+    rt = T.RayTracer(W, H)
+    rt.load_scene(scene_text("globes"), 0.25, asset_dir=SCENES)
+    r = rt.renderer
+    full = r.render_rows_host(0, H)
+    band = band or -(-H // world)
+    slot_rows = D.rows_per_rank(H, world, layout, band)
+    gath = torch.zeros((world * slot_rows, W, 3), dtype=torch.uint8, device="cuda")
+    for rank in range(world):
+        y_first, band_rows, pitch, n_bands = D.band_params(H, world, rank, layout, band)
+        r.render_row_bands(y_first, band_rows, pitch, n_bands, gath[rank * slot_rows:(rank + 1) * slot_rows])
+    frame = D.assemble(gath, H, world, layout, band)                     # rt_assemble_row_bands_rgb8
+    ref = D.assemble_reference(gath, H, world, layout, band)             # torch restatement
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy(), full)
+    assert np.array_equal(ref.cpu().numpy(), full)
+
+
+def test_assemble_rgb8_kernel_random(T):
+    import torch
+    from tinyraytracerinrust_amd import distributed as D
+    for W, H, world, band in [(3840, 2160, 8, 8), (33, 61, 3, 5)]:
+        slot_rows = D.rows_per_rank(H, world, "cyclic", band)
+        g = torch.randint(0, 256, (world * slot_rows, W, 3), dtype=torch.uint8, device="cuda")
+        want = D.assemble_reference(g, H, world, "cyclic", band).cpu()
+        got = D.assemble(g, H, world, "cyclic", band).cpu()
+        assert torch.equal(got, want)
+        assert (got[..., 3] == 255).all()

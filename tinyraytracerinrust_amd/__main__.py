@@ -110,14 +110,14 @@ def render(a) -> dict:
         times["render_ms"] = (time.perf_counter() - t0) * 1e3
     else:
         band = a.band if a.layout == "cyclic" else -(-H // world)
-        slot = torch.zeros((D.rows_per_rank(H, world, a.layout, band), W, 4), dtype=torch.uint8, device=dev)
+        slot = torch.zeros((D.rows_per_rank(H, world, a.layout, band), W, 3), dtype=torch.uint8, device=dev)   # packed RGB8
         y_first, band_rows, pitch, n_bands = D.band_params(H, world, rank, a.layout, band)
         if n_bands:
             r.render_row_bands(y_first, band_rows, pitch, n_bands, slot, max_depth=a.depth)
         torch.cuda.synchronize(dev)
         times["render_ms"] = (time.perf_counter() - t0) * 1e3
         t0 = time.perf_counter()
-        gath = torch.empty((world * slot.shape[0], W, 4), dtype=torch.uint8, device=dev)
+        gath = torch.empty((world * slot.shape[0], W, 3), dtype=torch.uint8, device=dev)
         dist.all_gather_into_tensor(gath, slot)
         frame = D.assemble(gath, H, world, a.layout, band)
         torch.cuda.synchronize(dev)

@@ -1017,7 +1017,7 @@ template <bool REFR, bool F64, bool CAL = false, bool FC = false>
 __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(RT_WAVES(REFR)))) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
                                                           int n_rows, int max_depth, uint8_t* __restrict__ out,
                                                           size_t stride, const int32_t* __restrict__ order,
-                                                          uint32_t* __restrict__ cost) {
+                                                          uint32_t* __restrict__ cost, int rgb) {
 #ifdef RT_DIAG_LDS                       // diagnostic builds only: cap occupancy with an LDS pad
   __shared__ volatile char rt_pad[RT_DIAG_LDS];
   if (threadIdx.x == 0) rt_pad[0] = 0;
@@ -1051,6 +1051,9 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   if constexpr (F64) {
     double* o = (double*)row + (size_t)x * 4;
     o[0] = c.r; o[1] = c.g; o[2] = c.b; o[3] = 1.0;                        // alpha is 1 after any colour op
+  } else if (rgb) {                                                        // packed RGB8 (band gathers)
+    uint8_t* o = row + (size_t)x * 3;
+    o[0] = (uint8_t)to_u8(c.r); o[1] = (uint8_t)to_u8(c.g); o[2] = (uint8_t)to_u8(c.b);
   } else {
     ((uint32_t*)row)[x] = to_u8(c.r) | (to_u8(c.g) << 8) | (to_u8(c.b) << 16) | (255u << 24);
   }
@@ -1075,7 +1078,7 @@ template <bool F64, bool CAL = false, bool FC = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_DEFERRED))) void
 render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth,
                             uint8_t* __restrict__ out, size_t stride, const int32_t* __restrict__ order,
-                            uint32_t* __restrict__ cost) {
+                            uint32_t* __restrict__ cost, int rgb) {
   __shared__ ShadowWin win;
   const int lane = threadIdx.x & 63;
   const uint32_t e = CAL || !order ? blockIdx.x : (uint32_t)order[blockIdx.x];
@@ -1101,6 +1104,9 @@ render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_p
     if constexpr (F64) {
       double* o = (double*)row + (size_t)x * 4;
       o[0] = c.r; o[1] = c.g; o[2] = c.b; o[3] = 1.0;
+    } else if (rgb) {
+      uint8_t* o = row + (size_t)x * 3;
+      o[0] = (uint8_t)to_u8(c.r); o[1] = (uint8_t)to_u8(c.g); o[2] = (uint8_t)to_u8(c.b);
     } else {
       ((uint32_t*)row)[x] = to_u8(c.r) | (to_u8(c.g) << 8) | (to_u8(c.b) << 16) | (255u << 24);
     }
@@ -1414,6 +1420,21 @@ __global__ __launch_bounds__(256) void assemble_bands_kernel(const uint8_t* __re
   }
 }
 
+// The same placement from packed RGB8 slot rows (3 bytes per pixel, rt_render_row_bands_rgb8) into
+// RGBA8 frame rows with A = 255: the all-gather moves 3/4 of the bytes.  One workgroup per row,
+// one pixel per thread and iteration (3 byte loads, one 4-byte store).
+__global__ __launch_bounds__(256) void assemble_bands_rgb_kernel(const uint8_t* __restrict__ g, size_t gstride,
+                                                                 int world, int slot_rows, int band, int width,
+                                                                 uint8_t* __restrict__ f, size_t fstride) {
+  const int y = blockIdx.x, b = y / band;
+  const uint8_t* s = g + ((size_t)(b % world) * slot_rows + (size_t)(b / world) * band + y % band) * gstride;
+  uint32_t* d = (uint32_t*)(f + (size_t)y * fstride);
+  for (int x = threadIdx.x; x < width; x += blockDim.x) {
+    const uint8_t* p = s + (size_t)x * 3;
+    d[x] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | (255u << 24);
+  }
+}
+
 }  // namespace
 
 // ====================================================================== device context
@@ -1675,7 +1696,7 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
 }
 
 static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_t band_pitch, uint32_t n_bands,
-                        int32_t max_depth, void* out, size_t stride, void* stream, bool f64) {
+                        int32_t max_depth, void* out, size_t stride, void* stream, bool f64, bool rgb = false) {
   if (!c || !out) return fail(RT_ERR_INVALID, "null argument");
   if (!c->uploaded) return fail(RT_ERR_INVALID, "no scene uploaded to this context");
   if (band_rows == 0 || n_bands == 0) return RT_OK;
@@ -1684,7 +1705,8 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   const uint64_t n_rows64 = (uint64_t)band_rows * n_bands;
   if (n_rows64 > (1u << 24)) return fail(RT_ERR_INVALID, "too many rows");
   const uint32_t n_rows = (uint32_t)n_rows64;
-  size_t row_bytes = (size_t)c->dev.width * (f64 ? 32 : 4);
+  size_t row_bytes = (size_t)c->dev.width * (f64 ? 32 : rgb ? 3 : 4);
+  const int rgbi = rgb && !f64 ? 1 : 0;
   if (stride < row_bytes) return fail(RT_ERR_INVALID, "row stride %zu < %zu", stride, row_bytes);
   if (max_depth < 0) max_depth = c->max_depth;
   if (max_depth > RT_MAX_DEPTH_CAP) return fail(RT_ERR_UNSUPPORTED, "max_depth %d > %d", max_depth, RT_MAX_DEPTH_CAP);
@@ -1748,22 +1770,22 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   RT_HIP(hipEventRecord(c->ev0, st));
 #define RT_LAUNCH_ROWS(R, F)                                                                                  \
   if (calibrate && fc) hipLaunchKernelGGL((render_rows_kernel<R, F, true, true>), grid, block, 0, st, c->dev, a0, a1, \
-                                          a2, a3, max_depth, target, tstride, order, cost);                       \
+                                          a2, a3, max_depth, target, tstride, order, cost, rgbi);                       \
   else if (calibrate) hipLaunchKernelGGL((render_rows_kernel<R, F, true, false>), grid, block, 0, st, c->dev, a0, a1, \
-                                         a2, a3, max_depth, target, tstride, order, cost);                        \
+                                         a2, a3, max_depth, target, tstride, order, cost, rgbi);                        \
   else if (fc) hipLaunchKernelGGL((render_rows_kernel<R, F, false, true>), grid, block, 0, st, c->dev, a0, a1, a2, a3, \
-                                  max_depth, target, tstride, order, cost);                                       \
+                                  max_depth, target, tstride, order, cost, rgbi);                                       \
   else hipLaunchKernelGGL((render_rows_kernel<R, F, false, false>), grid, block, 0, st, c->dev, a0, a1, a2, a3,   \
-                          max_depth, target, tstride, order, cost);
+                          max_depth, target, tstride, order, cost, rgbi);
 #define RT_LAUNCH_DEFERRED(F)                                                                                   \
   if (calibrate && fc) hipLaunchKernelGGL((render_rows_deferred_kernel<F, true, true>), grid, dim3(64), 0, st, c->dev, \
-                                          a0, a1, a2, a3, max_depth, target, tstride, order, cost);             \
+                                          a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);             \
   else if (calibrate) hipLaunchKernelGGL((render_rows_deferred_kernel<F, true, false>), grid, dim3(64), 0, st, c->dev, \
-                                         a0, a1, a2, a3, max_depth, target, tstride, order, cost);              \
+                                         a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);              \
   else if (fc) hipLaunchKernelGGL((render_rows_deferred_kernel<F, false, true>), grid, dim3(64), 0, st, c->dev, a0, \
-                                  a1, a2, a3, max_depth, target, tstride, order, cost);                         \
+                                  a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);                         \
   else hipLaunchKernelGGL((render_rows_deferred_kernel<F, false, false>), grid, dim3(64), 0, st, c->dev, a0, a1, a2, \
-                          a3, max_depth, target, tstride, order, cost);
+                          a3, max_depth, target, tstride, order, cost, rgbi);
   const bool fc = c->dev.colour_fast != 0 && fast_clamp_enabled();
   if (refr && f64) { RT_LAUNCH_ROWS(true, true) }
   else if (refr) { RT_LAUNCH_ROWS(true, false) }
@@ -1881,6 +1903,11 @@ int rt_render_row_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   return launch_bands(c, y_first, band_rows, band_pitch, n_bands, max_depth, rgba8, row_stride_bytes, stream, false);
 }
 
+int rt_render_row_bands_rgb8(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_t band_pitch, uint32_t n_bands,
+                             int32_t max_depth, uint8_t* rgb8, size_t row_stride_bytes, void* stream) {
+  return launch_bands(c, y_first, band_rows, band_pitch, n_bands, max_depth, rgb8, row_stride_bytes, stream, false, true);
+}
+
 int rt_render_rows(rt_ctx* c, uint32_t y0, uint32_t y1, int32_t max_depth, uint8_t* rgba8,
                    size_t row_stride_bytes, void* stream) {
   return launch_rows(c, y0, y1, max_depth, rgba8, row_stride_bytes, stream, false);
@@ -1908,6 +1935,27 @@ int rt_assemble_row_bands(const uint8_t* gathered, size_t gathered_stride, uint3
   const bool v16 = (((uintptr_t)gathered | (uintptr_t)frame | gathered_stride | frame_stride | row_bytes) & 15) == 0;
   hipLaunchKernelGGL(assemble_bands_kernel, dim3(height), dim3(256), 0, (hipStream_t)stream, gathered, gathered_stride,
                      (int)world, (int)slot_rows, (int)band_rows, row_bytes, frame, frame_stride, v16 ? 1 : 0);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}
+
+int rt_assemble_row_bands_rgb8(const uint8_t* gathered, size_t gathered_stride, uint32_t world, uint32_t slot_rows,
+                               uint32_t band_rows, uint32_t height, uint32_t width, uint8_t* frame, size_t frame_stride,
+                               void* stream) {
+  if (!gathered || !frame) return fail(RT_ERR_INVALID, "null argument");
+  if (world == 0 || band_rows == 0) return fail(RT_ERR_INVALID, "world and band_rows must be > 0");
+  if (height == 0 || width == 0) return RT_OK;
+  if (height > (1u << 24) || width > (1u << 24)) return fail(RT_ERR_INVALID, "frame too large");
+  const uint64_t bands = ((uint64_t)height + band_rows - 1) / band_rows, per_rank = (bands + world - 1) / world;
+  if ((uint64_t)slot_rows < per_rank * band_rows)
+    return fail(RT_ERR_INVALID, "slot of %u rows holds fewer than %llu bands of %u rows", slot_rows,
+                (unsigned long long)per_rank, band_rows);
+  if (slot_rows > (1u << 24) || (uint64_t)slot_rows * world > (1u << 30)) return fail(RT_ERR_INVALID, "slot too large");
+  if (gathered_stride < (size_t)width * 3 || frame_stride < (size_t)width * 4) return fail(RT_ERR_INVALID, "row stride < row bytes");
+  if ((((uintptr_t)frame) | frame_stride) & 3) return fail(RT_ERR_INVALID, "frame rows must be 4-byte aligned");
+  if (!is_device_ptr(gathered) || !is_device_ptr(frame)) return fail(RT_ERR_INVALID, "frame assembly takes device pointers");
+  hipLaunchKernelGGL(assemble_bands_rgb_kernel, dim3(height), dim3(256), 0, (hipStream_t)stream, gathered, gathered_stride,
+                     (int)world, (int)slot_rows, (int)band_rows, (int)width, frame, frame_stride);
   RT_HIP(hipGetLastError());
   return RT_OK;
 }

@@ -70,18 +70,40 @@ def render_local(render_rows: Callable[[int, int, torch.Tensor], None], height: 
 
 def assemble(gathered: torch.Tensor, height: int, world: int, layout: str, band: int,
              out: torch.Tensor = None) -> torch.Tensor:
-    """gathered: (world * slot_rows, W, 4) in rank order -> (H, W, 4) frame.
+    """gathered: (world * slot_rows, W, 4) RGBA8 or (world * slot_rows, W, 3) packed RGB8 slots in
+    rank order -> (H, W, 4) RGBA8 frame (A = 255 for RGB slots).
 
     On a GPU tensor this is ONE launch of the library's row-placement kernel
-    (rt_assemble_row_bands, 16-byte row copies); on CPU tensors (gloo) the torch restatement
-    assemble_reference below, which the GPU tests compare it with."""
+    (rt_assemble_row_bands, 16-byte row copies; rt_assemble_row_bands_rgb8 for RGB slots); on CPU
+    tensors (gloo) the torch restatement assemble_reference below, which the GPU tests compare it
+    with."""
     if not gathered.is_cuda:
         return assemble_reference(gathered, height, world, layout, band, out)
     slot_rows = gathered.shape[0] // world
+    band_rows = slot_rows if layout == "contiguous" else band
+    if gathered.shape[-1] == 3:
+        return _assemble_device_rgb(gathered, height, world, slot_rows, band_rows, out)
     if layout == "contiguous" and out is None:
         return gathered[:height]                                  # already in frame order: a view
-    band_rows = slot_rows if layout == "contiguous" else band
     return _assemble_device(gathered, height, world, slot_rows, band_rows, out)
+
+
+def _assemble_device_rgb(gathered: torch.Tensor, height: int, world: int, slot_rows: int, band_rows: int,
+                         out: torch.Tensor = None) -> torch.Tensor:
+    import ctypes
+    from . import _lib
+    W = gathered.shape[1]
+    if out is None:
+        out = torch.empty((height, W, 4), dtype=torch.uint8, device=gathered.device)
+    if tuple(out.shape) != (height, W, 4) or out.dtype != torch.uint8 or out.device != gathered.device:
+        raise ValueError(f"frame tensor {tuple(out.shape)} {out.dtype} does not match {(height, W, 4)} uint8")
+    if not (gathered[0].is_contiguous() and out[0].is_contiguous()):
+        raise ValueError("rows of the gathered buffer and the frame must be contiguous")
+    st = torch.cuda.current_stream(gathered.device).cuda_stream
+    _lib.check(_lib.lib().rt_assemble_row_bands_rgb8(
+        ctypes.c_void_p(gathered.data_ptr()), gathered.stride(0), world, slot_rows, band_rows, height, W,
+        ctypes.c_void_p(out.data_ptr()), out.stride(0), ctypes.c_void_p(st)))
+    return out
 
 
 def _assemble_device(gathered: torch.Tensor, height: int, world: int, slot_rows: int, band_rows: int,
@@ -110,6 +132,10 @@ def assemble_reference(gathered: torch.Tensor, height: int, world: int, layout: 
     frame is a permutation: view (world, bands_per_rank, band, ...) -> swap the first two axes ->
     first H rows."""
     slot_rows = gathered.shape[0] // world
+    if gathered.shape[-1] == 3:                                    # packed RGB slots -> RGBA, A = 255
+        rgba = torch.full(gathered.shape[:-1] + (4,), 255, dtype=gathered.dtype, device=gathered.device)
+        rgba[..., :3] = gathered
+        gathered = rgba
     if layout == "contiguous":
         frame = gathered[:height]
         if out is not None:

@@ -209,12 +209,13 @@ class Renderer:
 
     def render_row_bands(self, y_first: int, band_rows: int, band_pitch: int, n_bands: int, out,
                          max_depth: int = -1, stream=None) -> None:
-        """rt_render_row_bands into a device uint8 tensor ``out`` of >= n_bands*band_rows rows."""
+        """rt_render_row_bands into a device uint8 tensor ``out`` of >= n_bands*band_rows rows: RGBA8
+        (rows, W, 4), or packed RGB8 (rows, W, 3) through rt_render_row_bands_rgb8."""
         import torch
         st = stream if stream is not None else torch.cuda.current_stream(torch.device("cuda", self.device))
-        check(lib().rt_render_row_bands(self.h, y_first, band_rows, band_pitch, n_bands, max_depth,
-                                        ctypes.c_void_p(out.data_ptr()), out.stride(0) * out.element_size(),
-                                        ctypes.c_void_p(st.cuda_stream)))
+        fn = lib().rt_render_row_bands_rgb8 if out.shape[-1] == 3 else lib().rt_render_row_bands
+        check(fn(self.h, y_first, band_rows, band_pitch, n_bands, max_depth, ctypes.c_void_p(out.data_ptr()),
+                 out.stride(0) * out.element_size(), ctypes.c_void_p(st.cuda_stream)))
 
     def render_rows_host(self, y0: int, y1: int, max_depth: int = -1, f64: bool = False) -> np.ndarray:
         """Synchronous render into a host numpy array (the library stages through HBM)."""
