@@ -87,6 +87,30 @@ EDGE_SCENES = {
     "signed_zero_xf": "translate(0, 5, 0) draw(sphere(<0, 0, 0>, 30, red, 0.3))\n"
                       "translate(0, -30, 0) draw(cube(<0, 0, 0>, 20, red * 0.5, 0.5))\n"
                       "scale(1, 0.5, 1) draw(sphere(<30, 0, 0>, 10, red * 0.2, 0.4, 0.5))",
+    # concentric sphere leaves under one transform (RtLeaf::share_prev: a chain of three in a
+    # transparent object, so the refraction kernel's shared terms run), concentric spheres under
+    # DIFFERENT transforms (no sharing), and planes along x, tilted, and rotated (only the
+    # untransformed axis-aligned ones take RtLeaf::plane_axis)
+    "shared_spheres_planes": (
+        'rotate(0.2, 0.5, 0) do\n'
+        '  a = sphere(<-10, 0, 0>, 15)\n'
+        '  b = sphere(<-10, 0, 0>, 13)\n'
+        '  c = sphere(<-10, 0, 0>, 11)\n'
+        "  draw(csg(csg(a, b, 'difference'), c, 'union', rgb(0.9, 0.4, 0.2), 0.3, 0.6))\n"
+        'end\n'
+        'rotate(0, 0.7, 0) do\n'
+        '  d = sphere(<20, 5, 0>, 9)\n'
+        'end\n'
+        'e = sphere(<20, 5, 0>, 7)\n'
+        "draw(csg(d, e, 'difference', rgb(0.2, 0.8, 0.9), 0.4, 0.5))\n"
+        'draw(plane(<1, 0, 0>, 45, rgb(0.2, 0.6, 0.2), 0.3))\n'
+        'draw(plane(<0, 0, -1>, 80, rgb(0.7, 0.7, 0.7), 0.2))\n'
+        'draw(plane(<0.3, 1, 0>, 30, rgb(0.6, 0.6, 0.3), 0.3))\n'
+        'rotate(0.3, 0, 0) do\n'
+        '  draw(plane(<0, 1, 0>, 60, rgb(0.5, 0.1, 0.6), 0.4))\n'
+        'end\n'
+        'set camera(<0, 10, -85>)\n'
+    ),
 }
 
 

@@ -99,6 +99,15 @@ constexpr double EPS = RT_EPSILON;
                                     // the registers that let reflection-only scenes run 7 waves/SIMD
                                     // (profiles/r01ad_ab_light_group.txt)
 #endif
+#ifndef RT_PLANE_AXIS
+#define RT_PLANE_AXIS 1             // axis-aligned planes: one product per dot in the traversals
+#endif
+#ifndef RT_SPHERE_SHARE
+#define RT_SPHERE_SHARE 1           // concentric sphere leaves with one transform share their ray terms
+#endif
+#ifndef RT_REUSE_SDIR
+#define RT_REUSE_SDIR 1             // one light direction per (hit, light) for the shadow ray and Lambert
+#endif
 constexpr double PI_D = 3.14159265358979323846;   // std::f64::consts::PI
 
 struct V3 { double x, y, z; };
@@ -221,8 +230,26 @@ __device__ void sphere_uv(cptr<RtLeaf> L, V3 p, double* u, double* v) {
 // `fin` = wave_finite(ro, rd): selects the exact short forms for identity / diagonal-affine
 // leaves (rt_blob.h).  POS: the caller accepts only t > EPS (the traversals), so a plane whose
 // distance is provably <= 0 from the signs alone skips its division (see the plane branch).
+// SphereShare: a traversal's per-lane record of the last sphere leaf's ray terms.  A sphere leaf
+// with RtLeaf::share_prev (the previous leaf of its object is a sphere with a bit-identical
+// inverse transform and centre, and is evaluated by every lane that evaluates this one, see
+// rt_blob.h) has the same object-space ray, hence the same 1/|d|, v.dn and v.v: only r^2 differs,
+// so it reuses them and skips the transform, the length, the division and two dot products.
+struct SphereShare { double il, vd, vv; };
+
 template <bool POS = false>
-__device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, bool fin, double* t0, double* t1) {
+__device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, bool fin, double* t0, double* t1,
+                                               SphereShare* sh = nullptr) {
+#if RT_SPHERE_SHARE
+  if (sh && L->share_prev) {                                               // math_shapes.rs:42-62
+    const double sum = sh->vd * sh->vd - (sh->vv - L->r2);
+    if (sum < 0.0) return 0;
+    const double sq = sqrt(sum);
+    *t0 = (-sh->vd + sq) * sh->il;
+    *t1 = (-sh->vd - sq) * sh->il;
+    return 2;
+  }
+#endif
   V3 o, d;
   if (L->xdiag == RT_XF_IDENTITY && fin) {
     o = ro;
@@ -240,7 +267,9 @@ __device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, boo
     double il = 1.0 / len(d);
     V3 dn = scale(d, il);
     double vd = dot(v, dn);
-    double sum = vd * vd - (dot(v, v) - L->r2);
+    const double vv = dot(v, v);
+    if (sh) *sh = {il, vd, vv};
+    double sum = vd * vd - (vv - L->r2);
     if (sum < 0.0) return 0;
     double sq = sqrt(sum);
     *t0 = (-vd + sq) * il;
@@ -249,9 +278,21 @@ __device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, boo
   }
   if (k == RT_N_PLANE) {                                                   // :168-180
     V3 pn = ld3(L->pnorm);
-    double v_d = dot(pn, d);
+    double v_d, num;
+#if RT_PLANE_AXIS
+    const int ax = L->plane_axis;
+    if (POS && fin && ax >= 0) {               // axis-aligned normal: one product (rt_blob.h)
+      if (ax == 0) { v_d = pn.x * d.x; num = pn.x * o.x; }
+      else if (ax == 1) { v_d = pn.y * d.y; num = pn.y * o.y; }
+      else { v_d = pn.z * d.z; num = pn.z * o.z; }
+    } else
+#endif
+    {
+      v_d = dot(pn, d);
+      num = dot(pn, o);
+    }
     if (v_d != 0.0) {
-      const double num = dot(pn, o) + L->pl[0][3];
+      num = num + L->pl[0][3];
       // t = -num * (1/v_d) is > 0 only if num and v_d have opposite signs (rounding keeps signs;
       // 1/v_d may overflow to +-inf, never to 0).  Otherwise t is <= 0, -0 or NaN: never > EPS.
       if (POS && !((num > 0.0 && v_d < 0.0) || (num < 0.0 && v_d > 0.0))) return 0;
@@ -361,11 +402,15 @@ __device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) 
 // Nearest hit over all objects in draw order: accept d if d > EPS && d < nearest
 // (raytracer.rs:141-150).  The acceptance test is pure, so it runs BEFORE the (pure) CSG
 // filter: candidates that cannot win never pay for the sibling is_inside tests.
+// SHARE: concentric sphere leaves reuse their ray terms (SphereShare); it keeps three doubles live
+// across the leaf loop, so only kernels with register headroom take it (see trace()).
+template <bool SHARE = false>
 __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0) {
   [[maybe_unused]] const int cb = cat * 9;
   CNT(cb + 0);
   double best = INFINITY;
   int bobj = -1;
+  SphereShare shr = {0.0, 0.0, 0.0};
   const CullRay cr = cull_ray(ro, rd);
   const bool fin = wave_finite(ro, rd);
   int resume = 0;
@@ -398,7 +443,7 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
       CNT(cb + 4);
       CNT(cb + 5 + (L->kind == RT_N_SPHERE ? 0 : L->kind == RT_N_PLANE ? 1 : 2));
       double t0 = 0.0, t1 = 0.0;
-      int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1);
+      int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1, SHARE ? &shr : nullptr);
       const bool filtered = L->prog_end != L->prog_begin;
       if (filtered && ((n >= 1 && t0 > EPS && t0 < best) || (n >= 2 && t1 > EPS))) CNT(cb + 8);
       if (n >= 1 && t0 > EPS && t0 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) {
@@ -416,10 +461,12 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
 // Product of the transparencies of every filtered hit with EPS < d < dist (raytracer.rs:181-197).
 // Early-out once the product is exactly 0 (it stays 0: every factor is finite, checked on the
 // host), objects of transparency exactly 1.0 are skipped (x * 1.0 == x).
+template <bool SHARE = false>
 __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
   [[maybe_unused]] constexpr int cb = 18;
   CNT(cb + 0);
   double tr = 1.0;
+  SphereShare shr = {0.0, 0.0, 0.0};
   const CullRay cr = cull_ray(p, dir);
   const bool fin = wave_finite(p, dir);
   const double tmax = cull_tmax(dist);
@@ -453,7 +500,7 @@ __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
       CNT(cb + 4);
       CNT(cb + 5 + (L->kind == RT_N_SPHERE ? 0 : L->kind == RT_N_PLANE ? 1 : 2));
       double t0 = 0.0, t1 = 0.0;
-      int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1);
+      int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1, SHARE ? &shr : nullptr);
       const bool filtered = L->prog_end != L->prog_begin;
       if (filtered && ((n >= 1 && t0 > EPS && t0 < dist) || (n >= 2 && t1 > EPS && t1 < dist))) CNT(cb + 8);
       if (n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) {
@@ -668,6 +715,11 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
   double fRP[REFR ? RT_MAX_DEPTH_CAP : 1];
   int fPend[REFR ? RT_MAX_DEPTH_CAP : 1];
   constexpr bool RECORD = !std::is_same<Rec, NoRec>::value;
+  // Shared sphere terms (SphereShare) in the refraction kernels only: at 4 waves/SIMD they have
+  // the registers (104 -> 116 VGPRs, no spill; spinning_globes 1080p 4.8 % faster), while the
+  // reflection-only megakernel at 5 waves spills 14 more VGPRs and runs 6 % slower on 4K globes
+  // (profiles/r02am_ab.txt).
+  constexpr bool SHARE = REFR && RT_SPHERE_SHARE;
   int fSlot[RECORD ? RT_MAX_DEPTH_CAP : 1];
   [[maybe_unused]] int ray_type = 0, slot = 0;                  // RayType::NormalRay
   int sp = 0, depth = 0;
@@ -677,7 +729,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
     bool descend = false;
     double t_hit;
     PROF_T0(p0);
-    const int oi = nearest_hit(S, ro, rd, &t_hit, trip == 0 ? 0 : 1);
+    const int oi = nearest_hit<SHARE>(S, ro, rd, &t_hit, trip == 0 ? 0 : 1);
     PROF_ADD(trip == 0 ? 0 : 1, p0);
     ++trip;
     PROF_T0(p1);
@@ -695,6 +747,38 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
       // normal / UV / material and the per-light Lambert terms are formed afterwards: far fewer
       // registers live across the traversals.  Light accumulation order is unchanged.
       bool have_shading = false;
+#if RT_LIGHT_GROUP == 1 && RT_REUSE_SDIR
+      // One light at a time: the unit vector towards the light is the shadow ray's direction
+      // (:176-178) AND the Lambert term's `sdir` (:203-205), the same operations on the same
+      // operands, so it is formed once and kept for the Lambert term.
+#pragma unroll 1
+      for (int k = 0; k < S.n_lights; ++k) {
+        cptr<RtLight> lt = &S.lights[k];
+        const V3 lv = sub(ld3(lt->p), p);
+        const double ll = len(lv);
+        const V3 sdir = scale(lv, 1.0 / ll);                               // normalized(lv)
+#ifdef RT_ABLATE_NO_SHADOWS
+        const double t = lv.x > 1e300 ? 0.5 : 1.0;
+#else
+        PROF_T0(p2);
+        const double t = shadow_transparency<SHARE>(S, p, sdir, ll);       // :176-197
+        PROF_ADD(2, p2);
+#endif
+        if (!have_shading) {
+          PROF_T0(p3);
+          shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
+          PROF_ADD(3, p3);
+          L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));                      // ambient (:172)
+          have_shading = true;
+        }
+        if (t == 0.0) continue;                                            // :199-227
+        double ang = rt_acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
+        if (ang >= PI_D / 2.0) ang = PI_D - ang;
+        const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
+        const Col lc = intensify<FC>(intensify<FC>(Col{lt->col[0], lt->col[1], lt->col[2]}, inten), t);
+        L = cadd<FC>(L, cmul<FC>(c, lc));
+      }
+#else
       for (int base = 0; base < S.n_lights; base += RT_LIGHT_GROUP) {
         double tr[RT_LIGHT_GROUP];
 #pragma unroll
@@ -707,7 +791,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
           const double t = lv.x > 1e300 ? 0.5 : 1.0;
 #else
           PROF_T0(p2);
-          const double t = shadow_transparency(S, p, normalized(lv), len(lv));   // :176-197
+          const double t = shadow_transparency<SHARE>(S, p, normalized(lv), len(lv));   // :176-197
           PROF_ADD(2, p2);
 #endif
 #pragma unroll
@@ -732,6 +816,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
           L = cadd<FC>(L, cmul<FC>(c, lc));
         }
       }
+#endif
       if (!have_shading) {
         shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
         L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));

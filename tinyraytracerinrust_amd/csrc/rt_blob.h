@@ -76,8 +76,22 @@ struct alignas(16) RtLeaf {
                         // RT_XF_IDENTITY: inv is the identity and inv_o = 0: no transform at all
   int32_t n_lit;        // >= 0: the filter program is the conjunction of n_lit literals below
   int32_t lit[RT_MAX_LITS];   // literal = 2 * leaf + want: leaf[lit >> 1].is_inside(p) == (lit & 1)
-  int32_t pad[2];
+  int32_t plane_axis;   // untransformed plane leaf: 0/1/2 when pnorm has exactly one nonzero (finite) component; else -1
+  int32_t share_prev;   // sphere leaf: 1 = the previous leaf of the object is a sphere with a bit-identical
+                        // inverse transform (inv, inv_o, xdiag) and centre, and every traversal that
+                        // evaluates this leaf has evaluated that one first (see below)
 };
+// share_prev: the traversals evaluate an object's leaves in order, each unless its own box test
+// culls it (only when the object has leaf_cull).  The host sets share_prev only if the previous
+// leaf is never skipped when this one is evaluated: the object has no per-leaf culling, or the
+// previous leaf's cull is NONE, or both are BOX tests with this leaf's box inside the previous
+// one's.  The box test's slab times are monotone in the bounds and tmax never grows along the
+// loop, so a ray that passes the inner box has passed the outer one.
+// plane_axis = a: dot(pnorm, v) = (n0*v.x + n1*v.y) + n2*v.z equals n_a * v_a for FINITE v whenever
+// n_a * v_a != 0 (the other two products are signed zeros); when n_a * v_a is +-0 the sum is some
+// +-0 too.  The plane test only asks `v_d != 0` of the direction term and, for traversals (t > EPS
+// wanted), the strict signs of num = dot(pnorm, o) + d and v_d, which a signed zero never passes,
+// so the short form decides every traversal test exactly (render_kernels.hip leaf_candidates).
 // Literal form: most CSG filters (every ancestor requiring an intersection / difference sibling
 // inside, or a union sibling outside) are a plain conjunction of single-leaf is_inside tests;
 // the host rewrites the postfix program into at most RT_MAX_LITS literals (n_lit = -1: keep the

@@ -122,6 +122,7 @@ static inline V apply_dir(const double m[16], V v) { return sub(apply(m, v), app
 // ---------------------------------------------------------------- flattening
 static void leaf_common(const rt_transformation& t, RtLeaf* L) {
   memset(L, 0, sizeof *L);
+  L->plane_axis = -1;
   memcpy(L->inv, t.inverse, 12 * sizeof(double));
   memcpy(L->mat, t.matrix, 12 * sizeof(double));
   V io = apply(t.inverse, {0.0, 0.0, 0.0});
@@ -168,6 +169,15 @@ static int make_leaf(const ShapeRec& s, RtLeaf* L) {
       plane_into(s.t, s.normal[0], s.normal[1], s.normal[2], s.distance, L->pl[0], L->pn[0]);
       V pn = normalized({s.normal[0], s.normal[1], s.normal[2]});   // intersects (:169)
       L->pnorm[0] = pn.x; L->pnorm[1] = pn.y; L->pnorm[2] = pn.z;
+      {
+        const double n[3] = {pn.x, pn.y, pn.z};
+        int nz = 0, ax = -1;
+        for (int i = 0; i < 3; ++i)
+          if (n[i] != 0.0) { ++nz; ax = i; }
+        // untransformed planes only: the kernel's `fin` is the finiteness of the WORLD ray, which is
+        // the object-space ray only under the identity (a transform may overflow to inf)
+        L->plane_axis = (nz == 1 && std::isfinite(n[ax]) && L->xdiag == RT_XF_IDENTITY) ? ax : -1;
+      }
       break;
     }
     case SHAPE_CUBE: {                                          // math_shapes.rs:228-244
@@ -509,6 +519,18 @@ int flatten(const rt_scene& s, FlatScene* out) {
         ++n_leaf_boxes_tighter;
     }
     ob.leaf_cull = n_leaf_boxes_tighter > 0;
+    // concentric sphere leaves with one transform share their ray terms (rt_blob.h share_prev)
+    for (int32_t l = ob.leaf_begin + 1; l < ob.leaf_begin + ob.leaf_count; ++l) {
+      RtLeaf& L = f.leaves[l];
+      const RtLeaf& P = f.leaves[l - 1];
+      L.share_prev = 0;
+      if (L.kind != RT_N_SPHERE || P.kind != RT_N_SPHERE || L.xdiag != P.xdiag) continue;
+      if (memcmp(L.inv, P.inv, sizeof L.inv) || memcmp(L.inv_o, P.inv_o, sizeof L.inv_o) || memcmp(L.c, P.c, sizeof L.c))
+        continue;
+      bool inner = L.cull == RT_CULL_BOX && P.cull == RT_CULL_BOX;
+      for (int i = 0; i < 3 && inner; ++i) inner = P.blo[i] <= L.blo[i] && L.bhi[i] <= P.bhi[i];
+      if (!ob.leaf_cull || P.cull == RT_CULL_NONE || L.cull == RT_CULL_ALWAYS || inner) L.share_prev = 1;
+    }
     const rt_material& m = o.mat;
     ob.textured = m.texture >= 0;
     ob.tex = m.texture >= 0 ? m.texture : 0;
@@ -549,8 +571,9 @@ int flatten(const rt_scene& s, FlatScene* out) {
               ob.blo[0], ob.blo[1], ob.blo[2], ob.bhi[0], ob.bhi[1], ob.bhi[2], ob.leaf_count, ob.leaf_cull);
       for (int l = ob.leaf_begin; l < ob.leaf_begin + ob.leaf_count; ++l) {
         const RtLeaf& L = f.leaves[l];
-        fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d lits %d xdiag %d\n", l, L.kind, L.cull,
-                L.blo[0], L.blo[1], L.blo[2], L.bhi[0], L.bhi[1], L.bhi[2], L.prog_end - L.prog_begin, L.n_lit, L.xdiag);
+        fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d lits %d xdiag %d share %d axis %d\n", l, L.kind,
+                L.cull, L.blo[0], L.blo[1], L.blo[2], L.bhi[0], L.bhi[1], L.bhi[2], L.prog_end - L.prog_begin, L.n_lit,
+                L.xdiag, L.share_prev, L.plane_axis);
       }
     }
   }

@@ -1,0 +1,12 @@
+# A/B: light direction reused for the Lambert term (RT_REUSE_SDIR) and axis-aligned plane tests
+# (RT_PLANE_AXIS), interleaved in one process; then the parity tests on the product library.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out
+B=tinyraytracerinrust_amd/build
+P=tinyraytracerinrust_amd/librt_mi355x.so
+timeout -k 10 300 python tools/ab_interleaved.py $B/librt_mi355x_base.so $B/librt_mi355x_sdir.so $B/librt_mi355x_plane.so $P --reps 12 --burst 10 > $O/r02al_ab.txt 2>&1 || exit 1
+timeout -k 10 300 python tools/ab_interleaved.py $B/librt_mi355x_base.so $P --reps 12 --burst 10 --size 1920x1080 --scene spinning_globes --time 0.3 >> $O/r02al_ab.txt 2>&1 || exit 1
+cat $O/r02al_ab.txt
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fastclamp.py -x -q --timeout 120 --timeout-method thread -m gpu > $O/r02al_pytest.txt 2>&1 || { tail -30 $O/r02al_pytest.txt; exit 1; }
+tail -3 $O/r02al_pytest.txt
