@@ -56,7 +56,7 @@ __device__ unsigned long long g_rt_prof[8];
 // tests, leaf evaluations (all / sphere / plane / cube), CSG filter calls; lane-events, one atomic
 // per wave per event.
 #ifdef RT_COUNT
-__device__ unsigned long long g_rt_cnt[32];
+__device__ unsigned long long g_rt_cnt[64];
 #define CNT(i)                                                                          \
   do {                                                                                  \
     const unsigned long long m_ = __ballot(1);                                          \
@@ -408,6 +408,7 @@ template <bool SHARE = false>
 __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0) {
   [[maybe_unused]] const int cb = cat * 9;
   CNT(cb + 0);
+  CNTW(32 + cat);
   double best = INFINITY;
   int bobj = -1;
   SphereShare shr = {0.0, 0.0, 0.0};
@@ -441,6 +442,7 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
         if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, cull_tmax(best))) continue;
       }
       CNT(cb + 4);
+      CNTW(35 + cat);
       CNT(cb + 5 + (L->kind == RT_N_SPHERE ? 0 : L->kind == RT_N_PLANE ? 1 : 2));
       double t0 = 0.0, t1 = 0.0;
       int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1, SHARE ? &shr : nullptr);
@@ -465,6 +467,7 @@ template <bool SHARE = false>
 __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
   [[maybe_unused]] constexpr int cb = 18;
   CNT(cb + 0);
+  CNTW(34);
   double tr = 1.0;
   SphereShare shr = {0.0, 0.0, 0.0};
   const CullRay cr = cull_ray(p, dir);
@@ -498,6 +501,7 @@ __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
         if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
       }
       CNT(cb + 4);
+      CNTW(37);
       CNT(cb + 5 + (L->kind == RT_N_SPHERE ? 0 : L->kind == RT_N_PLANE ? 1 : 2));
       double t0 = 0.0, t1 = 0.0;
       int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1, SHARE ? &shr : nullptr);
@@ -1682,10 +1686,10 @@ static size_t put(std::vector<uint8_t>& blob, const std::vector<T>& v) {
 extern "C" {
 
 #ifdef RT_COUNT
-__attribute__((visibility("default"))) int rt_diag_cnt(unsigned long long* out32) {
+__attribute__((visibility("default"))) int rt_diag_cnt(unsigned long long* out64) {
   if (hipDeviceSynchronize() != hipSuccess) return RT_ERR_DEVICE;
-  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_rt_cnt), 32 * sizeof(unsigned long long)) != hipSuccess) return RT_ERR_DEVICE;
-  static const unsigned long long zero[32] = {0};
+  if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_rt_cnt), 64 * sizeof(unsigned long long)) != hipSuccess) return RT_ERR_DEVICE;
+  static const unsigned long long zero[64] = {0};
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_rt_cnt), zero, sizeof(zero)) != hipSuccess) return RT_ERR_DEVICE;
   return RT_OK;
 }

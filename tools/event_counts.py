@@ -16,7 +16,7 @@ from tinyraytracerinrust_amd import _lib
 S = os.path.join(ROOT, "tests", "golden", "scenes")
 L = _lib.lib()
 L.rt_diag_cnt.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-buf = (ctypes.c_ulonglong * 32)()
+buf = (ctypes.c_ulonglong * 64)()
 EV = ["rays", "obj box tests", "obj entered", "leaf box tests", "leaf evals", "  sphere", "  plane", "  cube",
       "filter calls"]
 # usage: event_counts.py [SCENE WxH TIME DEPTH[,DEPTH...]]   (default: globes 3840x2160 0 10,0)
@@ -42,3 +42,8 @@ for W, H, d in [(W0, H0, dd) for dd in DEPTHS]:
             v = buf[c * 9 + i]
             print(f"    {e:16s} {v:14d}  [{v / rays:7.3f}]")
     print(f"  shade waterfall iterations (per wave): {buf[27]}  waves {W * H // 64}")
+    # SIMD lane utilisation: lane-events / (wave-events x 64)
+    for c, nm in enumerate(["primary", "secondary", "shadow"]):
+        wc, wl = buf[32 + c], buf[35 + c]
+        print(f"  {nm:9s} traversal calls: {buf[c * 9] / max(1, 64 * wc):.3f} of lanes active; "
+              f"leaf evaluations: {buf[c * 9 + 4] / max(1, 64 * wl):.3f} of lanes active ({wc} wave calls, {wl} wave leaf evals)")
