@@ -338,6 +338,13 @@ struct Flattener {
   }
 };
 
+// Two sphere leaves with bit-identical inverse transforms and centres: the same object-space ray
+// for every world ray, hence the same 1/|d|, v.dn and v.v (rt_blob.h share_prev).
+static bool shares_sphere_terms(const RtLeaf& L, const RtLeaf& P) {
+  return L.kind == RT_N_SPHERE && P.kind == RT_N_SPHERE && L.xdiag == P.xdiag && !memcmp(L.inv, P.inv, sizeof L.inv) &&
+         !memcmp(L.inv_o, P.inv_o, sizeof L.inv_o) && !memcmp(L.c, P.c, sizeof L.c);
+}
+
 // ---------------------------------------------------------------- hit-filter literal form
 // Rewrite a leaf's postfix filter program [b, e) into a conjunction of literals (2*leaf + want)
 // when every REQUIRE reduces to one: v == 1 of AND / ANDNOT and v == 0 of OR distribute over
@@ -381,6 +388,45 @@ static int filter_literals(const std::vector<RtProg>& prog, int32_t b, int32_t e
   if (uniq.size() > RT_MAX_LITS) return -1;
   for (size_t i = 0; i < uniq.size(); ++i) lits[i] = uniq[i];
   return (int32_t)uniq.size();
+}
+
+// Concentric sphere leaves with one transform share their ray terms (rt_blob.h share_prev).  The
+// refraction kernels use the shared terms (render_kernels.hip trace: SHARE), so in scenes with a
+// transparent object per-leaf box tests that cannot cull, or that cost what the shared quadratic
+// costs, are dropped as well.  `uncond`: the leaf is evaluated whenever its object is entered.
+static void share_sphere_terms(FlatScene& f, RtObject* ob) {
+  if (ob->leaf_cull && f.any_transparent) {
+    bool prev_uncond = false;
+    for (int32_t l = ob->leaf_begin; l < ob->leaf_begin + ob->leaf_count; ++l) {
+      RtLeaf& L = f.leaves[l];
+      bool uncond = L.cull == RT_CULL_NONE;
+      // the first leaf's test repeats the object's (same box, same tmax: no hit accepted between)
+      if (l == ob->leaf_begin && L.cull == RT_CULL_BOX && ob->cull == RT_CULL_BOX &&
+          !memcmp(L.blo, ob->blo, sizeof L.blo) && !memcmp(L.bhi, ob->bhi, sizeof L.bhi)) {
+        L.cull = RT_CULL_NONE;
+        uncond = true;
+      }
+      // a sharing sphere whose predecessor always runs: its test costs what the shared quadratic
+      // costs (a ray that misses the sphere stops at `sum < 0`), so it runs unconditionally too
+      if (l > ob->leaf_begin && prev_uncond && L.cull == RT_CULL_BOX && shares_sphere_terms(L, f.leaves[l - 1])) {
+        L.cull = RT_CULL_NONE;
+        uncond = true;
+      }
+      prev_uncond = uncond;
+    }
+    bool any_test = false;
+    for (int32_t l = ob->leaf_begin; l < ob->leaf_begin + ob->leaf_count; ++l) any_test |= f.leaves[l].cull != RT_CULL_NONE;
+    ob->leaf_cull = any_test;
+  }
+  for (int32_t l = ob->leaf_begin + 1; l < ob->leaf_begin + ob->leaf_count; ++l) {
+    RtLeaf& L = f.leaves[l];
+    const RtLeaf& P = f.leaves[l - 1];
+    L.share_prev = 0;
+    if (!shares_sphere_terms(L, P)) continue;
+    bool inner = L.cull == RT_CULL_BOX && P.cull == RT_CULL_BOX;
+    for (int i = 0; i < 3 && inner; ++i) inner = P.blo[i] <= L.blo[i] && L.bhi[i] <= P.bhi[i];
+    if (!ob->leaf_cull || P.cull == RT_CULL_NONE || L.cull == RT_CULL_ALWAYS || inner) L.share_prev = 1;
+  }
 }
 
 // ---------------------------------------------------------------- object hierarchy
@@ -519,18 +565,6 @@ int flatten(const rt_scene& s, FlatScene* out) {
         ++n_leaf_boxes_tighter;
     }
     ob.leaf_cull = n_leaf_boxes_tighter > 0;
-    // concentric sphere leaves with one transform share their ray terms (rt_blob.h share_prev)
-    for (int32_t l = ob.leaf_begin + 1; l < ob.leaf_begin + ob.leaf_count; ++l) {
-      RtLeaf& L = f.leaves[l];
-      const RtLeaf& P = f.leaves[l - 1];
-      L.share_prev = 0;
-      if (L.kind != RT_N_SPHERE || P.kind != RT_N_SPHERE || L.xdiag != P.xdiag) continue;
-      if (memcmp(L.inv, P.inv, sizeof L.inv) || memcmp(L.inv_o, P.inv_o, sizeof L.inv_o) || memcmp(L.c, P.c, sizeof L.c))
-        continue;
-      bool inner = L.cull == RT_CULL_BOX && P.cull == RT_CULL_BOX;
-      for (int i = 0; i < 3 && inner; ++i) inner = P.blo[i] <= L.blo[i] && L.bhi[i] <= P.bhi[i];
-      if (!ob.leaf_cull || P.cull == RT_CULL_NONE || L.cull == RT_CULL_ALWAYS || inner) L.share_prev = 1;
-    }
     const rt_material& m = o.mat;
     ob.textured = m.texture >= 0;
     ob.tex = m.texture >= 0 ? m.texture : 0;
@@ -545,6 +579,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
     if (m.texture < 0 && !(nonneg(m.color[0]) && nonneg(m.color[1]) && nonneg(m.color[2]))) f.colour_fast = 0;
     f.objects.push_back(ob);
   }
+  for (RtObject& ob : f.objects) share_sphere_terms(f, &ob);
   build_hierarchy(&f);
   for (const LightRec& l : s.lights) {
     RtLight L;
