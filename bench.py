@@ -621,7 +621,7 @@ def anim_main(a, json_out, rank, world, local, dev, multi):
             "peak": FP64_VECTOR_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4) if achieved else None,
-            "traffic": None,
+            "traffic": load_traffic(a.config, 1, "contiguous"),     # HBM bytes per frame (PMC, profiles/)
             "kernel": "render_rows_kernel<REFR=true>",
             "streams": K,
             "achieved_basis": "kernel event time" if K == 1 else "step wall time (frames overlap on the streams)",

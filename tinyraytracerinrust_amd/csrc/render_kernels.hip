@@ -829,8 +829,14 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
     if (oi < 0) {
       C = {0.0, 0.0, 0.0};                                               // Color::BLACK (:152-160)
     } else {
-      const V3 nd = scale(rd, -1.0);                                      // :230-235
-      const bool inside = inside_test(dot(nd, nrm) / (len(nd) * len(nrm)));
+      // The inside test (:230-235) only matters for a hit that spawns a ray: one with
+      // depth < max_depth and a reflectivity or a transparency.  Other hits skip its division
+      // and square roots (the values it would give are never read).
+      bool inside = false;
+      if (depth < max_depth && (refl != 0.0 || (REFR && transp != 0.0))) {
+        const V3 nd = scale(rd, -1.0);
+        inside = inside_test(dot(nd, nrm) / (len(nd) * len(nrm)));
+      }
       const V3 n2 = inside ? scale(nrm, -1.0) : nrm;
       const double r1 = inside ? 1.45 : 1.0, r2 = inside ? 1.0 : 1.45;
       bool tir = false;
@@ -956,8 +962,11 @@ __device__ Col trace_deferred(const DS& S, V3 ro, V3 rd, int max_depth, bool val
       double transp, refl;
       shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);                    // :163-170
       // inside test (:230-235), exactly as trace(); no transparent object: no refraction, no TIR
-      const V3 nd = scale(rd, -1.0);
-      const bool inside = inside_test(dot(nd, nrm) / (len(nd) * len(nrm)));
+      bool inside = false;                                                 // needed only if a ray may spawn
+      if (depth < max_depth && refl != 0.0) {
+        const V3 nd = scale(rd, -1.0);
+        inside = inside_test(dot(nd, nrm) / (len(nd) * len(nrm)));
+      }
       const bool do_refl = depth < max_depth && refl != 0.0 && !inside;    // :267
       hP[nh][0] = p.x; hP[nh][1] = p.y; hP[nh][2] = p.z;
       hN[nh][0] = nrm.x; hN[nh][1] = nrm.y; hN[nh][2] = nrm.z;
