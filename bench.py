@@ -271,7 +271,13 @@ def main():
     # 0.182 / 0.093 ms, profiles/r02x_inflight_*.txt).
     if K >= 3:
         rend.set_kernel("mega")
-    rstreams = [stream] if K == 1 else [torch.cuda.Stream(dev) for _ in range(K)]
+    # Each in-flight frame on a stream with a hardware queue of its own (rt_stream_create): torch's
+    # pool streams share the process's 4 hardware queues, and two renders whose streams land on
+    # one queue serialise -- a rank's N = 8 share with K = 4 measured 0.072 or 0.118 ms depending
+    # on which pool streams it got, 0.075-0.079 every time on own-queue streams
+    # (profiles/r02ba_streams.txt).
+    hw = [] if K == 1 else [T.HwStream(local) for _ in range(K)]
+    rstreams = [stream] if K == 1 else [h.torch for h in hw]
     ch = 3 if a.gather == "rgb" else 4
     slots = [torch.zeros((slot_rows, W, ch), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
     gath = [torch.zeros((world * slot_rows, W, ch), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
@@ -404,6 +410,7 @@ def main():
             "collective": None if not multi else f"all_gather_into_tensor (RCCL) of {a.gather.upper()}8 band slots" + (
                 ", overlapped with later frames" if overlap else ""),
             "frames_in_flight": K,
+            "streams": "current stream" if K == 1 else f"{K} streams, each with its own hardware queue (rt_stream_create)",
             "kernel": "megakernel (rt_ctx_set_option)" if K >= 3 else "library's choice (auto)",
             "frame_bytes": W * H * 4,
         },
@@ -543,7 +550,8 @@ def anim_main(a, json_out, rank, world, local, dev, multi):
     prep_ms = (time.perf_counter() - t0) * 1e3 / max(1, len(mine))
     outs = [torch.zeros((H, W, 4), dtype=torch.uint8, device=dev) for _ in mine]
     K = max(1, a.streams)
-    streams = [torch.cuda.current_stream(dev)] if K == 1 else [torch.cuda.Stream(dev) for _ in range(K)]
+    hw = [] if K == 1 else [T.HwStream(local) for _ in range(K)]      # own hardware queues (main())
+    streams = [torch.cuda.current_stream(dev)] if K == 1 else [h.torch for h in hw]
     torch.cuda.synchronize(dev)
 
     def step(evs=None):

@@ -10,6 +10,7 @@ from .raytracer import (  # noqa: F401
     MAX_FRAMES,
     ORTHO_SCALE,
     AntiAliaser,
+    HwStream,
     OrthoAxes,
     RAY_RECORD_DTYPE,
     RayDebugger,
@@ -26,7 +27,7 @@ from .raytracer import (  # noqa: F401
 )
 
 __all__ = [
-    "RtError", "lib", "MAX_FRAMES", "ORTHO_SCALE", "AntiAliaser", "OrthoAxes", "RAY_RECORD_DTYPE", "RayDebugger", "MatrixTransformation", "RayTracer", "Renderer", "Scene",
+    "RtError", "lib", "MAX_FRAMES", "ORTHO_SCALE", "AntiAliaser", "HwStream", "OrthoAxes", "RAY_RECORD_DTYPE", "RayDebugger", "MatrixTransformation", "RayTracer", "Renderer", "Scene",
     "TransformationStack", "device_count", "read_png_rgba8", "solid_material", "textured_material",
     "write_png",
 ]

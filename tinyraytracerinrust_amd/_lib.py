@@ -97,6 +97,8 @@ SIGNATURES = {
     "rt_ctx_last_kernel_ms": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
     "rt_ctx_synchronize": (_I, [_P]),
     "rt_ctx_set_option": (_I, [_P, ctypes.c_int32, ctypes.c_int32]),
+    "rt_stream_create": (_I, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "rt_stream_destroy": (_I, [_P]),
     "rt_ctx_free": (None, [_P]),
     "rt_write_png": (_I, [ctypes.c_char_p, _P, _U32, _U32, ctypes.c_size_t, _I]),
     "rt_read_png_rgba8": (_I, [ctypes.c_char_p, ctypes.POINTER(_P), ctypes.POINTER(_U32),

@@ -2304,6 +2304,29 @@ int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
   return RT_OK;
 }
 
+int rt_stream_create(int device, void** stream) {
+  if (!stream) return fail(RT_ERR_INVALID, "null argument");
+  int n_dev = 0;
+  RT_HIP(hipGetDeviceCount(&n_dev));
+  if (device < 0 || device >= n_dev) return fail(RT_ERR_INVALID, "device %d of %d", device, n_dev);
+  RT_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  RT_HIP(hipGetDeviceProperties(&prop, device));
+  // every CU enabled: the mask only buys the stream a hardware queue of its own
+  std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0xFFFFFFFFu);
+  if (prop.multiProcessorCount % 32) mask.back() = (1u << (prop.multiProcessorCount % 32)) - 1u;
+  hipStream_t st = nullptr;
+  RT_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+  *stream = st;
+  return RT_OK;
+}
+
+int rt_stream_destroy(void* stream) {
+  if (!stream) return fail(RT_ERR_INVALID, "null stream");
+  RT_HIP(hipStreamDestroy((hipStream_t)stream));
+  return RT_OK;
+}
+
 int rt_ctx_synchronize(rt_ctx* c) {
   if (!c) return fail(RT_ERR_INVALID, "null context");
   RT_HIP(hipSetDevice(c->device));

@@ -511,3 +511,28 @@ def device_count() -> int:
     n = ctypes.c_int()
     check(lib().rt_device_count(ctypes.byref(n)))
     return n.value
+
+
+class HwStream:
+    """A HIP stream on a hardware queue of its own (rt_stream_create), usable as a torch stream
+    (``.torch``, a torch.cuda.ExternalStream).  Renders meant to overlap go on such streams: plain
+    torch / HIP streams share the process's few hardware queues, and two renders on one queue run
+    one after the other (include/rt_abi.h rt_stream_create)."""
+
+    def __init__(self, device: int = 0):
+        import torch
+        h = ctypes.c_void_p()
+        check(lib().rt_stream_create(device, ctypes.byref(h)))
+        self.handle = h.value
+        self.torch = torch.cuda.ExternalStream(self.handle, device=torch.device("cuda", device))
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            lib().rt_stream_destroy(ctypes.c_void_p(self.handle))
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
