@@ -340,3 +340,29 @@ def test_assemble_rgb8_kernel_random(T):
         got = D.assemble(g, H, world, "cyclic", band).cpu()
         assert torch.equal(got, want)
         assert (got[..., 3] == 255).all()
+
+
+def test_own_queue_streams_overlapping_frames(T):
+    """Frames rendered concurrently on streams with their own hardware queue (rt_stream_create /
+    HwStream, as bench.py's frames in flight) equal the synchronous render, including the
+    ordered launches that follow the calibration."""
+    import torch
+    W, H = 640, 480
+    rt = T.RayTracer(W, H)
+    rt.load_scene(scene_text("globes"), 0.1, asset_dir=SCENES)
+    r = rt.renderer
+    want = r.render_rows(0, H)
+    torch.cuda.synchronize()
+    hs = [T.HwStream(0) for _ in range(4)]
+    outs = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(8)]
+    r.set_kernel("mega")
+    for i, o in enumerate(outs):
+        r.render_rows(0, H, out=o, stream=hs[i % 4].torch)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, want)
+    for h in hs:
+        h.close()
+    from tinyraytracerinrust_amd import _lib
+    with pytest.raises(T.RtError):
+        _lib.check(T.lib().rt_stream_destroy(None))
