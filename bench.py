@@ -93,6 +93,8 @@ def parse():
                          "frame's tail is its costliest "
                          "tiles, so a lone frame leaves the GPU partly idle at its end (a rank's "
                          "share is floored by its slowest tile, so one frame alone leaves the GPU idle)")
+    ap.add_argument("--pool-streams", action="store_true",
+                    help="diagnostic: frames in flight on torch pool streams instead of own-queue streams")
     ap.add_argument("--streams", type=int, default=2,
                     help="anim120: frames dealt round-robin over this many HIP streams so independent "
                          "frames' kernels overlap (one 1080p frame does not fill the GPU to its end)")
@@ -276,22 +278,27 @@ def main():
     # one queue serialise -- a rank's N = 8 share with K = 4 measured 0.072 or 0.118 ms depending
     # on which pool streams it got, 0.075-0.079 every time on own-queue streams
     # (profiles/r02ba_streams.txt).
-    hw = [] if K == 1 else [T.HwStream(local) for _ in range(K)]
-    rstreams = [stream] if K == 1 else [h.torch for h in hw]
+    hw = [] if K == 1 or a.pool_streams else [T.HwStream(local) for _ in range(K)]
+    rstreams = [stream] if K == 1 else [h.torch for h in hw] if hw else [torch.cuda.Stream(dev) for _ in range(K)]
     ch = 3 if a.gather == "rgb" else 4
     slots = [torch.zeros((slot_rows, W, ch), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
     gath = [torch.zeros((world * slot_rows, W, ch), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else []
     frames = [frame] + [torch.zeros_like(frame) for _ in range(nbuf - 1)]
     free_ev = [None] * nbuf    # buffer b's last gather and assembly are done once this event fires
-    pending = []               # (work, buffer, stream) of gathers not yet assembled, oldest first
+    pending = []               # (work, buffer) of gathers not yet assembled, oldest first
+    # Assemblies run on a stream of their own: on a render stream an assembly would queue behind
+    # that stream's NEXT render, and the render after it (which waits for the buffer the assembly
+    # frees) could not start before the previous render ended -- the renders would serialise.
+    ahw = T.HwStream(local) if K > 1 and not a.pool_streams else None    # kept alive with the stream
+    astream = stream if K == 1 else (ahw.torch if ahw else torch.cuda.Stream(dev))
 
     def finish(p):
-        work, b, s = p
-        with torch.cuda.stream(s):
-            work.wait()                                   # s waits for the gather
+        work, b = p
+        with torch.cuda.stream(astream):
+            work.wait()                                   # astream waits for the gather
             D.assemble(gath[b], H, world, layout, band, out=frames[b])
             free_ev[b] = torch.cuda.Event()
-            free_ev[b].record(s)
+            free_ev[b].record(astream)
 
     def step(i, ev0=None, ev1=None):
         b = i % nbuf
@@ -310,7 +317,7 @@ def main():
             if multi:
                 work = dist.all_gather_into_tensor(gath[b], slots[b], async_op=True)   # after s's render
         if multi:
-            pending.append((work, b, s))
+            pending.append((work, b))
             while len(pending) > (K if overlap else 0):
                 finish(pending.pop(0))
 
@@ -410,7 +417,8 @@ def main():
             "collective": None if not multi else f"all_gather_into_tensor (RCCL) of {a.gather.upper()}8 band slots" + (
                 ", overlapped with later frames" if overlap else ""),
             "frames_in_flight": K,
-            "streams": "current stream" if K == 1 else f"{K} streams, each with its own hardware queue (rt_stream_create)",
+            "streams": "current stream" if K == 1 else f"{K} torch pool streams" if a.pool_streams else
+                       f"{K} streams, each with its own hardware queue (rt_stream_create)",
             "kernel": "megakernel (rt_ctx_set_option)" if K >= 3 else "library's choice (auto)",
             "frame_bytes": W * H * 4,
         },

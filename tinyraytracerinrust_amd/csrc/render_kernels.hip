@@ -2316,7 +2316,9 @@ int rt_stream_create(int device, void** stream) {
   std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0xFFFFFFFFu);
   if (prop.multiProcessorCount % 32) mask.back() = (1u << (prop.multiProcessorCount % 32)) - 1u;
   hipStream_t st = nullptr;
-  RT_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+  static const bool plain = getenv("RT_STREAM_PLAIN") != nullptr;   // diagnostic: a plain stream
+  if (plain) RT_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  else RT_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
   *stream = st;
   return RT_OK;
 }
