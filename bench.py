@@ -88,11 +88,11 @@ def parse():
                     help="CPU-baseline threads (0 = every core available to this process)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="frames whose renders may overlap, each on its own HIP stream (0 = 1 at N = 1, so the "
-                         "roofline's kernel time is one launch alone; 4 at N > 1, profiles/r02f_inflight.txt).  A "
-                         "frame's tail is its costliest "
-                         "tiles, so a lone frame leaves the GPU partly idle at its end (a rank's "
-                         "share is floored by its slowest tile, so one frame alone leaves the GPU idle)")
+                    help="frames whose renders may overlap, each on a stream with its own hardware queue "
+                         "(0 = 1 at N = 1, so the roofline's kernel time and the rocprof trace are of one launch "
+                         "alone; 4 at N > 1).  A frame's tail is its costliest tiles, so a lone frame leaves the "
+                         "GPU partly idle at its end; overlapping frames fill it (N = 1, --inflight 4: 4K globes "
+                         "+2.5 %%, 1080p d5 +37 %%, the sphere +52 %%, profiles/r02bg_inflight_n1.txt)")
     ap.add_argument("--pool-streams", action="store_true",
                     help="diagnostic: frames in flight on torch pool streams instead of own-queue streams")
     ap.add_argument("--streams", type=int, default=2,
