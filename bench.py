@@ -454,8 +454,9 @@ def main():
     if multi:
         line["distributed"] = {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(),
                                "rows_per_rank": rows_per_rank, "layout": layout, "band_rows": band,
-                               "frames_in_flight": K,
-            "kernel": "megakernel (rt_ctx_set_option)" if K >= 3 else "library's choice (auto)", "frame_check": frame_check}
+                               "frames_in_flight": K, "gather": a.gather,
+                               "kernel": "megakernel (rt_ctx_set_option)" if K >= 3 else "library's choice (auto)",
+                               "frame_check": frame_check}
     if world == 1 and not multi and not a.no_cpu_baseline:
         cb = cpu_baseline(text, W, H, t, depth, a.cpu_threads)
         cb["gpu_over_cpu"] = round(line["value"] / cb["value"], 1)

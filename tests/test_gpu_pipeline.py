@@ -1,0 +1,42 @@
+"""bench.py's N > 1 frame pipeline on one GPU: the RCCL path at world size 1 (torch.distributed.run,
+--force-collective) with 4 frames in flight on own-queue streams -- band renders, all-gathers of
+packed RGB8 (and RGBA8) slots, assemblies on their own stream, buffer reuse ordered by events.
+After its timed region bench.py compares EVERY frame buffer with a single-launch render of the
+frame and exits non-zero on a difference, so a stream-ordering or buffer-reuse mistake fails here.
+The tiled row loop this stands for is src/raydebugger/debug_window.rs:74-87."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from tests.conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("gather,layout", [("rgb", "cyclic"), ("rgba", "contiguous")])
+def test_collective_pipeline_frames_in_flight(gather, layout):
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--force-collective",
+           "--inflight", "4", "--steps", "12", "--warmup", "3", "--settle-ms", "0", "--no-cpu-baseline",
+           "--gather", gather, "--layout", layout]
+    p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd=ROOT, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([l for l in p.stdout.splitlines() if l.strip()][-1])
+    d = line["distributed"]
+    assert d["frames_in_flight"] == 4 and d["gather"] == gather
+    assert d["frame_check"].startswith("all 5 frame buffers")
+    assert "own hardware queue" in line["config"]["streams"]
