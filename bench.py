@@ -166,16 +166,34 @@ def load_flops(scene, W, H, t, depth):
         return json.load(f)
 
 
-def load_traffic(config, world, layout):
-    """HBM bytes per launch of the render kernel from the committed PMC summary (or None)."""
+def load_pmc(config, world, layout):
+    """The committed PMC summary entry of this config (profiles/pmc_summary.json, written by
+    tools/pmc_summary.py from rocprofv3 --pmc passes of this bench command), or {}."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
-        return None
+        return {}
     with open(path) as f:
         d = json.load(f)
     key = f"{config}/n{world}/{layout}"
-    e = d.get(key) or (d.get(f"{config}/n1/contiguous") if world == 1 else None)
-    return None if e is None else e.get("hbm_bytes_per_launch")
+    return d.get(key) or (d.get(f"{config}/n1/contiguous") if world == 1 else None) or {}
+
+
+def load_traffic(config, world, layout):
+    """HBM bytes per launch of the render kernel from the committed PMC summary (or None)."""
+    return load_pmc(config, world, layout).get("hbm_bytes_per_launch")
+
+
+def executed_fp64(config, world, layout, kernel_ms):
+    """The EXECUTED FP64 rate: (ADD + MUL + 2 FMA) wave-instructions x 64 per launch from the PMC
+    summary over this run's kernel time -- the hardware's view, next to `roofline.achieved` (the
+    reference algorithm's flops, of which exact culling skips about 60 %)."""
+    e = load_pmc(config, world, layout)
+    fl = e.get("executed_fp64_flops_per_launch")
+    if not fl or not kernel_ms:
+        return None
+    tf = fl / (kernel_ms * 1e-3) / 1e12
+    return {"tflops": round(tf, 3), "frac": round(tf / FP64_VECTOR_PEAK_TFLOPS, 4),
+            "flops_per_launch": fl, "pmc_tag": e.get("tag"), "valu_insts_per_wave": e.get("valu_insts_per_wave")}
 
 
 def cpu_baseline(text, W, H, t, depth, threads, target_s=1.0):
@@ -437,6 +455,7 @@ def main():
             "algorithmic_flops_per_launch": flops_launch,
             "frac_of_no_fma_ceiling": round(achieved / FP64_NO_FMA_TFLOPS, 4) if achieved else None,
             "no_fma_ceiling": FP64_NO_FMA_TFLOPS,
+            "executed_fp64": executed_fp64(a.config, world, layout, busy_ms),
         },
         "roofline_hbm": {
             "bound": "hbm",
@@ -645,6 +664,8 @@ def anim_main(a, json_out, rank, world, local, dev, multi):
             "kernel_ms_mean": round(sum(per_frame) / len(per_frame), 4),
             "kernel_ms_min": round(min(per_frame), 4),
             "kernel_ms_max": round(max(per_frame), 4),
+            "executed_fp64": executed_fp64(a.config, 1, "contiguous",
+                                           (sum(per_frame) / len(per_frame)) if K == 1 else elapsed * 1e3 / a.steps / len(mine)),
             "frac_of_no_fma_ceiling": round(achieved / FP64_NO_FMA_TFLOPS, 4) if achieved else None,
         },
         "rays": rays_line(fl, F * W * H * a.steps / elapsed),

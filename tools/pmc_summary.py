@@ -50,6 +50,10 @@ def main(tag="r01", config="globes4k", kernel="render_rows_kernel"):
     if "hbm_bytes_per_launch" in res:
         summ[f"{config}/n1/contiguous"] = {"tag": tag, "hbm_bytes_per_launch": res["hbm_bytes_per_launch"],
                                            "fetch_kb": mean["FETCH_SIZE"], "write_kb": mean["WRITE_SIZE"]}
+        if "executed_fp64_flops_per_launch" in res:
+            summ[f"{config}/n1/contiguous"]["executed_fp64_flops_per_launch"] = res["executed_fp64_flops_per_launch"]
+        if "SQ_INSTS_VALU" in mean and "SQ_WAVES" in mean:
+            summ[f"{config}/n1/contiguous"]["valu_insts_per_wave"] = round(mean["SQ_INSTS_VALU"] / mean["SQ_WAVES"], 1)
         with open(summ_path, "w") as f:
             json.dump(summ, f, indent=1)
     print(json.dumps(res, indent=1))
