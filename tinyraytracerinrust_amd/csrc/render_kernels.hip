@@ -693,11 +693,17 @@ typedef LDS_AS double lds_f64;
 #ifndef RT_LDS_FRAMES
 #define RT_LDS_FRAMES 2
 #endif
+// Refraction frames also carry the pending reflection ray (P, D, rp: 7 doubles); the first
+// KLR of them go to LDS after the KL colour frames, [frame][component][lane] likewise.
+#ifndef RT_LDS_RFRAMES
+#define RT_LDS_RFRAMES 1
+#endif
 
 // get_ray_color (raytracer.rs:132-287) for one primary ray, recursion unrolled onto a per-lane
 // frame stack.  REFR = the scene has a transparent object (refraction frames need more state).
-// KL > 0: frames 0..KL-1 of the stack are in LDS at lf[(f * 4 + c) * 64] (lf = this lane's slot).
-template <bool REFR, class Rec = NoRec, int KL = 0, bool FC = false>
+// KL > 0: frames 0..KL-1 of the stack are in LDS at lf[(f * 4 + c) * 64] (lf = this lane's slot);
+// KLR > 0 (REFR): the pending-reflection state of frames 0..KLR-1 at lf[(KL * 4 + f * 7 + c) * 64].
+template <bool REFR, class Rec = NoRec, int KL = 0, bool FC = false, int KLR = 0>
 __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, lds_f64* lf = nullptr) {
   double fA[RT_MAX_DEPTH_CAP][3];     // parent colour already intensified by (1 - w)
   double fW[RT_MAX_DEPTH_CAP];        // child weight w (transparency or reflectivity)
@@ -717,7 +723,24 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
   };
   double fP[REFR ? RT_MAX_DEPTH_CAP : 1][3], fD[REFR ? RT_MAX_DEPTH_CAP : 1][3];
   double fRP[REFR ? RT_MAX_DEPTH_CAP : 1];
-  int fPend[REFR ? RT_MAX_DEPTH_CAP : 1];
+  uint32_t pend = 0;                  // bit f: frame f's reflection ray is still to be traced
+  static_assert(RT_MAX_DEPTH_CAP <= 32, "pending-reflection bit mask");
+  auto put_rframe = [&](int f, V3 P, V3 D, double rp) {
+    if (KLR > 0 && f < KLR) {
+      lds_f64* q = lf + (KL * 4 + f * 7) * 64;
+      q[0] = P.x; q[64] = P.y; q[128] = P.z; q[192] = D.x; q[256] = D.y; q[320] = D.z; q[384] = rp;
+    } else {
+      fP[f][0] = P.x; fP[f][1] = P.y; fP[f][2] = P.z; fD[f][0] = D.x; fD[f][1] = D.y; fD[f][2] = D.z; fRP[f] = rp;
+    }
+  };
+  auto get_rframe = [&](int f, V3* P, V3* D, double* rp) {
+    if (KLR > 0 && f < KLR) {
+      const lds_f64* q = lf + (KL * 4 + f * 7) * 64;
+      *P = {q[0], q[64], q[128]}; *D = {q[192], q[256], q[320]}; *rp = q[384];
+    } else {
+      *P = {fP[f][0], fP[f][1], fP[f][2]}; *D = {fD[f][0], fD[f][1], fD[f][2]}; *rp = fRP[f];
+    }
+  };
   constexpr bool RECORD = !std::is_same<Rec, NoRec>::value;
   // Shared sphere terms (SphereShare) in the refraction kernels only: at 4 waves/SIMD they have
   // the registers (104 -> 116 VGPRs, no spill; spinning_globes 1080p 4.8 % faster), while the
@@ -848,13 +871,8 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
       if (do_refr && !tir) {
         put_frame(sp, intensify<FC>(L, 1.0 - transp), transp);
         if constexpr (REFR) {
-          fPend[sp] = do_refl ? 1 : 0;
-          if (do_refl) {
-            V3 rdir = reflect_dir(rd, n2);
-            fP[sp][0] = p.x; fP[sp][1] = p.y; fP[sp][2] = p.z;
-            fD[sp][0] = rdir.x; fD[sp][1] = rdir.y; fD[sp][2] = rdir.z;
-            fRP[sp] = rp;
-          }
+          pend = do_refl ? pend | (1u << sp) : pend & ~(1u << sp);
+          if (do_refl) put_rframe(sp, p, reflect_dir(rd, n2), rp);
         }
         if constexpr (RECORD) { fSlot[sp] = slot; ray_type = 2; }        // TransmissionRay
         ++sp;
@@ -864,7 +882,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
         descend = true;
       } else if (do_refl) {
         put_frame(sp, intensify<FC>(L, 1.0 - rp), rp);
-        if constexpr (REFR) fPend[sp] = 0;
+        if constexpr (REFR) pend &= ~(1u << sp);
         if constexpr (RECORD) { fSlot[sp] = slot; ray_type = 1; }        // ReflectionRay
         ++sp;
         rd = reflect_dir(rd, n2);
@@ -885,11 +903,11 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
       get_frame(f, &fa, &fw);
       const Col comb = cadd<FC>(fa, intensify<FC>(C, fw));
       if constexpr (REFR) {
-        if (fPend[f]) {                                                   // refraction done -> reflection
-          fPend[f] = 0;
-          put_frame(f, intensify<FC>(comb, 1.0 - fRP[f]), fRP[f]);
-          ro = {fP[f][0], fP[f][1], fP[f][2]};
-          rd = {fD[f][0], fD[f][1], fD[f][2]};
+        if ((pend >> f) & 1u) {                                           // refraction done -> reflection
+          pend &= ~(1u << f);
+          double frp;
+          get_rframe(f, &ro, &rd, &frp);
+          put_frame(f, intensify<FC>(comb, 1.0 - frp), frp);
           depth = sp;
           descend = true;
           if constexpr (RECORD) ray_type = 1;                              // ReflectionRay
@@ -1138,9 +1156,10 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   PROF_T0(p5);
   camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
 #if RT_LDS_FRAMES > 0
-  __shared__ double s_frames[RT_WG_WX * RT_WG_WY][RT_LDS_FRAMES * 4 * 64];   // frame stack, see trace()
+  constexpr int KLR = REFR ? RT_LDS_RFRAMES : 0;
+  __shared__ double s_frames[RT_WG_WX * RT_WG_WY][(RT_LDS_FRAMES * 4 + KLR * 7) * 64];   // frame stack, see trace()
   lds_f64* lf = (lds_f64*)&s_frames[wave][lane];
-  const Col c = trace<REFR, NoRec, RT_LDS_FRAMES, FC>(make_ds(S), ro, rd, max_depth, nullptr, lf);
+  const Col c = trace<REFR, NoRec, RT_LDS_FRAMES, FC, KLR>(make_ds(S), ro, rd, max_depth, nullptr, lf);
 #else
   const Col c = trace<REFR, NoRec, 0, FC>(make_ds(S), ro, rd, max_depth);
 #endif
