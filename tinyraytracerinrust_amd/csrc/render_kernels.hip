@@ -1413,17 +1413,21 @@ __global__ __launch_bounds__(256) void aa_expand_kernel(AaGrid G, uint32_t n, in
   for (int w = 0; w < RT_AA_HAVE_WORDS; ++w) h[w] = have[w];
 }
 
+// One-wave workgroups with the frame stack's first frames in LDS, as the row kernels.
 template <bool REFR, bool FC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES(REFR)))) void aa_trace_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES(REFR)))) void aa_trace_kernel(
     RtDevScene S, AaGrid G, const uint32_t* __restrict__ edges, const uint2* __restrict__ req, uint32_t n, int max_depth) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  constexpr int KLR = REFR ? RT_LDS_RFRAMES : 0;
+  __shared__ double s_frames[(RT_LDS_FRAMES * 4 + KLR * 7) * 64 + 1];
+  lds_f64* lf = (lds_f64*)&s_frames[threadIdx.x];
   if (i >= n) return;
   const uint2 r = req[i];
   const int x = edges[r.x] & 0xffff, y = edges[r.x] >> 16;
   const int sx = r.y & 0xff, sy = r.y >> 8, sz = G.size;
   V3 ro, rd;
   camera_ray(S.cam, (double)x + ((double)sx / (double)sz), (double)y + ((double)sy / (double)sz), &ro, &rd);   // :108-112
-  const Col c = trace<REFR, NoRec, 0, FC>(make_ds(S), ro, rd, max_depth);
+  const Col c = trace<REFR, NoRec, RT_LDS_FRAMES, FC, KLR>(make_ds(S), ro, rd, max_depth, nullptr, lf);
   G.col[(size_t)r.x * sz * sz + sx * sz + sy] = {c.r, c.g, c.b, 1.0};
 }
 
@@ -2157,9 +2161,9 @@ int rt_antialias(rt_ctx* c, const uint8_t* src_rgba8, size_t src_stride, double 
       if (n_req > cap) { err = fail(RT_ERR_DEVICE, "anti-aliasing request overflow (%u > %zu)", n_req, cap); break; }
       if (n_req == 0) break;
       rays += n_req;
-      const dim3 rg((n_req + 255) / 256);
+      const dim3 rg((n_req + 63) / 64);
       const bool fc = c->dev.colour_fast != 0 && fast_clamp_enabled();
-#define RT_LAUNCH_AA(R, F) hipLaunchKernelGGL((aa_trace_kernel<R, F>), rg, blk, 0, st, c->dev, G, edges, req, n_req, (int)max_depth)
+#define RT_LAUNCH_AA(R, F) hipLaunchKernelGGL((aa_trace_kernel<R, F>), rg, dim3(64), 0, st, c->dev, G, edges, req, n_req, (int)max_depth)
       if (c->dev.any_transparent && fc) RT_LAUNCH_AA(true, true);
       else if (c->dev.any_transparent) RT_LAUNCH_AA(true, false);
       else if (fc) RT_LAUNCH_AA(false, true);
