@@ -91,6 +91,8 @@ def test_no_gpu_fails_loudly():
     with pytest.raises(T.RtError) as e:
         T.Renderer(0)
     assert e.value.status == -5
+    with pytest.raises(T.RtError):                  # own-queue streams need a device too
+        T.HwStream(0)
 
 
 def _header_arity():
