@@ -117,3 +117,17 @@ def test_integration_rust_block_matches_header():
     hdr = _header_arity()
     assert sorted(hdr) == declared()
     assert rust == hdr
+
+
+def test_one_hip_runtime_per_process():
+    """Loading the library before torch must not start a second HIP runtime: torch wheels bundle
+    their own libamdhip64 / libhsa-runtime64, and with /opt/rocm's copies loaded first torch finds
+    no device.  _lib.lib() imports torch first, so exactly one libamdhip64 is mapped."""
+    import subprocess
+    import sys
+    code = ("import re, tinyraytracerinrust_amd as T; T.lib(); import torch; "
+            "m = open('/proc/self/maps').read(); "
+            "print(len(set(re.findall(r'(\\S*libamdhip64\\S*)', m))), len(set(re.findall(r'(\\S*libhsa-runtime64\\S*)', m))))")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.stdout.split() == ["1", "1"], p.stdout

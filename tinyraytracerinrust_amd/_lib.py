@@ -118,6 +118,14 @@ def lib() -> ctypes.CDLL:
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `make -C {HERE}` or __graft_entry__.build(); "
             "there is no CPU fallback for the render path")
+    # One HIP runtime per process: torch wheels bundle their own libamdhip64 / libhsa-runtime64
+    # (same SONAMEs as /opt/rocm's).  Loaded after torch, this library binds to torch's copies;
+    # loaded first, it would pull in /opt/rocm's, and torch's runtime, started later on top of an
+    # HSA runtime of another release, finds no device (torch.cuda.is_available() -> False).
+    try:
+        import torch  # noqa: F401
+    except ImportError:                               # a host without torch: /opt/rocm's runtime
+        pass
     handle = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(handle, name)

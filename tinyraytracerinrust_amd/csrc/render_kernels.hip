@@ -1965,10 +1965,14 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     }
     slot->deferred = eligible && (dmode == 1 || tail_bound);
     if (slot->deferred && n_tiles <= RT_SPLIT_TILE_MASK + 1) {
-      // Split the costliest tiles over P = 2, 4 or 8 waves (cost >= P * the median tile;
-      // RT_SPLIT_K overrides the factor 1, 0 disables): their shadow rays then spread over P x 64
-      // lanes.  Factor 1 / 1.5 / 2 / 3: N = 8 share 0.178 / 0.181 / 0.193 / 0.206 ms (r02f).
-      static const double split_k = [] { const char* e = getenv("RT_SPLIT_K"); return e ? atof(e) : 1.0; }();
+      // Split the costliest tiles over P = 2, 4 or 8 waves (cost >= k * P * the median tile):
+      // their shadow rays then spread over P x 64 lanes.  The factor k: 1 below 24000 tiles, 1.5
+      // above (env RT_SPLIT_K overrides both, 0 disables).  Swept at 1 / 1.25 / 1.5 / 2 / 3
+      // (profiles/r02bo_split_sweep.txt): the 4K N = 8 share (16320 tiles) 0.150 / 0.152 / 0.172 /
+      // 0.170 / 0.183 ms; the N = 4 share (32400 tiles) 0.209 / 0.192 / 0.190 / 0.200 / 0.232 ms;
+      // the whole 1080p d5 frame (32400 tiles) 0.208 / 0.189 / 0.184 / 0.181 / 0.225 ms.
+      static const double split_env = [] { const char* e = getenv("RT_SPLIT_K"); return e ? atof(e) : -1.0; }();
+      const double split_k = split_env >= 0.0 ? split_env : n_tiles < 24000 ? 1.0 : 1.5;
       std::vector<uint32_t> sorted_cost(h_cost);
       std::nth_element(sorted_cost.begin(), sorted_cost.begin() + n_tiles / 2, sorted_cost.end());
       const double med = std::max(1.0, (double)sorted_cost[n_tiles / 2]);
