@@ -948,6 +948,10 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
 #define RT_SH_TRCAP 128             // shadow results per round: hits per round = min(64, TRCAP / lights)
 #endif
 #define RT_SPLIT_TILE_MASK 0xFFFFFu   // order entries: tile index in bits 0-19 (split tiles: see below)
+#ifndef RT_SPLIT_MAX_LOG2
+#define RT_SPLIT_MAX_LOG2 3           // a costly tile goes to at most 2^3 = 8 waves (part: bits 20-23)
+#endif
+static_assert(RT_SPLIT_MAX_LOG2 <= 4, "split part index has 4 bits");
 struct ShadowWin {                  // LDS, one per wave: 2.5 KB
   double px[64], py[64], pz[64];
   double tr[RT_SH_TRCAP];
@@ -1184,7 +1188,7 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
 // costliest tiles split over P = 2, 4 or 8 waves: wave `part` renders pixels
 // [part * 64/P, (part + 1) * 64/P) of the tile on its first 64/P lanes and its other lanes only
 // trace shadow rays (phase 2), so a costly tile's shadow work spreads over P x 64 lanes and its
-// latency -- the launch's tail -- shrinks.  Order entry: tile | part << 20 | log2(P) << 23 (built
+// latency -- the launch's tail -- shrinks.  Order entry: tile | part << 20 | log2(P) << 24 (built
 // by launch_bands after the calibration launch).  A kernel of its own: the megakernel path and
 // this one in ONE kernel measured 3.4x slower than either (profiles/r02g_ab.txt: both paths' code
 // hot on one CU at once).
@@ -1200,8 +1204,8 @@ render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_p
   const int lane = threadIdx.x & 63;
   const uint32_t e = CAL || !order ? blockIdx.x : (uint32_t)order[blockIdx.x];
   const unsigned tile = e & RT_SPLIT_TILE_MASK;
-  const int lp = (int)((e >> 23) & 3u), per = 64 >> lp;
-  const int pix = (int)((e >> 20) & 7u) * per + lane;
+  const int lp = (int)((e >> 24) & 7u), per = 64 >> lp;
+  const int pix = (int)((e >> 20) & 15u) * per + lane;
   [[maybe_unused]] uint64_t t_start = 0;
   if constexpr (CAL) t_start = wall_clock64();
   const unsigned tiles_x = (unsigned)(S.width + 7) / 8;
@@ -1981,9 +1985,9 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
       for (size_t i = 0; i < n_tiles; ++i) {
         const uint32_t t = (uint32_t)h_order[i];
         int lp = 0;
-        while (split_k > 0.0 && lp < 3 && h_cost[t] >= split_k * med * (double)(2 << lp)) ++lp;
+        while (split_k > 0.0 && lp < RT_SPLIT_MAX_LOG2 && h_cost[t] >= split_k * med * (double)(2 << lp)) ++lp;
         for (int part = 0; part < (1 << lp); ++part)
-          split.push_back((int32_t)(t | ((uint32_t)part << 20) | ((uint32_t)lp << 23)));
+          split.push_back((int32_t)(t | ((uint32_t)part << 20) | ((uint32_t)lp << 24)));
       }
       if (split.size() > n_tiles) {
         int32_t* d = nullptr;
