@@ -93,6 +93,8 @@ def parse():
                          "alone; 4 at N > 1).  A frame's tail is its costliest tiles, so a lone frame leaves the "
                          "GPU partly idle at its end; overlapping frames fill it (N = 1, --inflight 4: 4K globes "
                          "+2.5 %%, 1080p d5 +37 %%, the sphere +52 %%, profiles/r02bg_inflight_n1.txt)")
+    ap.add_argument("--rccl-priority", default="normal", choices=["high", "normal"],
+                    help="priority of RCCL's stream (the all-gathers) relative to the render streams")
     ap.add_argument("--pool-streams", action="store_true",
                     help="diagnostic: frames in flight on torch pool streams instead of own-queue streams")
     ap.add_argument("--streams", type=int, default=2,
@@ -257,7 +259,12 @@ def main():
     dev = torch.device("cuda", local)
     multi = world > 1 or a.force_collective
     if multi:
-        dist.init_process_group("nccl", device_id=dev)
+        # The gathers run on RCCL's stream while later frames' renders fill every CU.  A
+        # high-priority RCCL stream (--rccl-priority high) measured 7 % slower per step on the RCCL
+        # path at world 1 (0.625 vs 0.582 ms, profiles/r02bw_rccl_priority.txt): normal by default.
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = a.rccl_priority == "high"
+        dist.init_process_group("nccl", device_id=dev, pg_options=opts)
 
     if a.config in ANIM:
         return anim_main(a, json_out, rank, world, local, dev, multi)
