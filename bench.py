@@ -84,6 +84,11 @@ def parse():
                     help="N > 1: do not overlap frame k's all-gather with frame k+1's render")
     ap.add_argument("--force-collective", action="store_true",
                     help="exercise the N > 1 path (process group, bands, all-gather) even at N = 1")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="diagnostic, not a measurement: run the N ranks' whole frame pipeline (HIP band renders, "
+                         "frames in flight, gathers, assembly kernel, per-rank frame checks) on ONE GPU -- every "
+                         "rank on device 0, the all-gather over gloo staged through host memory (RCCL refuses two "
+                         "ranks on one device).  The line carries no value")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0 = every core available to this process)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -255,10 +260,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: one rank per GPU")
+    rehearse = a.rehearse_one_gpu
+    if rehearse:
+        if a.config in ANIM or not launched:
+            raise SystemExit("--rehearse-one-gpu: a frame config under a launcher (--gpus N > 1 starts one)")
+        local = 0                        # every rank on the one GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    multi = world > 1 or a.force_collective
-    if multi:
+    multi = world > 1 or a.force_collective or rehearse
+    if rehearse:
+        dist.init_process_group("gloo")
+    elif multi:
         # The gathers run on RCCL's stream while later frames' renders fill every CU.  A
         # high-priority RCCL stream (--rccl-priority high) measured 7 % slower per step on the RCCL
         # path at world 1 (0.625 vs 0.582 ms, profiles/r02bw_rccl_priority.txt): normal by default.
@@ -340,7 +352,8 @@ def main():
             if ev1 is not None:
                 ev1.record(s)
             if multi:
-                work = dist.all_gather_into_tensor(gath[b], slots[b], async_op=True)   # after s's render
+                work = (HostGather(gath[b], slots[b], s) if rehearse else
+                        dist.all_gather_into_tensor(gath[b], slots[b], async_op=True))   # after s's render
         if multi:
             pending.append((work, b))
             while len(pending) > (K if overlap else 0):
@@ -382,7 +395,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if multi:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     kernel_ms = [s.elapsed_time(e) for s, e in evs]
@@ -477,6 +490,11 @@ def main():
         "frame_check": frame_check,
         "settle": settle,
     }
+    if rehearse:
+        line.update({"metric": "one-GPU rehearsal of the N-rank pipeline (not a measurement)", "value": None,
+                     "vs_baseline": None, "roofline": None, "roofline_hbm": None, "rays": None})
+        line["config"]["collective"] = "all_gather_into_tensor (gloo, staged through host memory) of " \
+                                       f"{a.gather.upper()}8 band slots; every rank on device 0"
     if multi:
         line["distributed"] = {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(),
                                "rows_per_rank": rows_per_rank, "layout": layout, "band_rows": band,
@@ -491,6 +509,25 @@ def main():
     json_out.flush()
     if multi:
         dist.destroy_process_group()
+
+
+class HostGather:
+    """--rehearse-one-gpu: the all-gather of one frame's band slots over gloo, staged through host
+    memory, with the interface bench's pipeline uses of an async RCCL work handle.  The slot is
+    copied out once the render stream `s` has finished it; wait() copies the gathered slots back to
+    the device on the CURRENT stream (the assembly stream), as RCCL's wait() orders that stream."""
+
+    def __init__(self, out, slot, s):
+        import torch
+        import torch.distributed as dist
+        s.synchronize()
+        self.out = out
+        self.host = torch.empty(out.shape, dtype=out.dtype)
+        self.work = dist.all_gather_into_tensor(self.host, slot.cpu(), async_op=True)
+
+    def wait(self):
+        self.work.wait()
+        self.out.copy_(self.host)
 
 
 def rays_line(fl, primary_per_s):

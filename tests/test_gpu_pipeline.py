@@ -40,3 +40,28 @@ def test_collective_pipeline_frames_in_flight(gather, layout):
     assert d["frames_in_flight"] == 4 and d["gather"] == gather
     assert d["frame_check"].startswith("all 5 frame buffers")
     assert "own hardware queue" in line["config"]["streams"]
+
+
+@pytest.mark.parametrize("world,inflight,layout", [(2, 0, "cyclic"), (4, 1, "cyclic"), (8, 0, "cyclic"),
+                                                    (3, 2, "contiguous")])
+def test_rehearsal_n_ranks_on_one_gpu(world, inflight, layout):
+    """The driver's N-GPU form (`python bench.py --gpus N`: bench.py starts its own N ranks) with
+    every rank on the one GPU of this box: N processes each render their cyclic bands with the
+    HIP library (megakernel with 4 frames in flight at the default K, the deferred-shadow kernel
+    with split tiles at K = 1 for N >= 4), the gathers run over a real 2..8-rank process group
+    (gloo, host-staged: RCCL refuses two ranks on one device), the assembly kernel builds every
+    frame, and EVERY rank checks every frame buffer against its own single-launch render."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
+           "--steps", "4", "--warmup", "2", "--settle-ms", "0", "--layout", layout, "--inflight", str(inflight)]
+    p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd=ROOT, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([l for l in p.stdout.splitlines() if l.strip()][-1])
+    assert line["value"] is None and line["n_gpus"] == world
+    d = line["distributed"]
+    assert d["backend"] == "gloo" and d["world_size_seen"] == world and d["layout"] == layout
+    assert sum(d["rows_per_rank"]) == line["config"]["height"] and len(d["rows_per_rank"]) == world
+    k = inflight or 4
+    assert d["frames_in_flight"] == k
+    assert d["frame_check"] == f"all {k + 1} frame buffers == single-launch render, on every rank"
