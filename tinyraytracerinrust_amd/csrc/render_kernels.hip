@@ -117,8 +117,71 @@ __device__ __forceinline__ V3 add(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.
 __device__ __forceinline__ V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
 __device__ __forceinline__ V3 scale(V3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
 __device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ double len(V3 a) { return sqrt(dot(a, a)); }
-__device__ __forceinline__ V3 normalized(V3 a) { return scale(a, 1.0 / len(a)); }
+// Correctly rounded sqrt(x) and 1/sqrt-derived reciprocals without their range handling.
+// For f64 `sqrt` and `/` the compiler emits (gfx950) scaled Newton sequences:
+//   sqrt(x): x scaled by 2^256 if x < 2^-767, y = rsq(x), g = x*y, h = 0.5*y, r = fma(-h,g,0.5),
+//            g = fma(g,r,g), h = fma(h,r,h), twice {d = fma(-g,g,x), g = fma(d,h,g)}, g scaled back,
+//            and x itself returned for +-0 / +inf (17 VALU instructions);
+//   a / b:   v_div_scale of b and of a, rcp, 4 Newton fmas, mul, fma, v_div_fmas, v_div_fixup (11).
+// For x in [2^-767, DBL_MAX] the scalings are by 2^0 and the class select returns g, so the
+// unscaled core below is the SAME operation sequence on the same values: bit-identical.  Then
+// l = sqrt(x) is in [2^-383.5, 2^512): for 1.0 / l v_div_scale scales neither operand (both
+// normal, exponent gap < 768, 1/l and the quotient normal), so v_div_fmas is a plain fma (VCC 0),
+// the mul by the numerator 1.0 is exact, and v_div_fixup returns its positive normal operand:
+// again the same values.  The range test is wave-uniform (one ballot), outside it the compiler's
+// sequences run.  RT_FAST_SQRT=0 restores the plain `sqrt` / `/` everywhere.
+#ifndef RT_FAST_SQRT
+#define RT_FAST_SQRT 1
+#endif
+__device__ __forceinline__ bool wave_sqrt_core_ok(double x) {
+  return __ballot(!(x >= 0x1p-767 && x <= 0x1.fffffffffffffp+1023)) == 0;
+}
+__device__ __forceinline__ double sqrt_core(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
+__device__ __forceinline__ double recip_core(double l) {     // 1.0 / l for l in [2^-384, 2^512]
+  const double nl = -l;
+  const double r = __builtin_amdgcn_rcp(l);
+  const double f0 = __builtin_fma(nl, r, 1.0);
+  const double f1 = __builtin_fma(r, f0, r);
+  const double f2 = __builtin_fma(nl, f1, 1.0);
+  const double f3 = __builtin_fma(f1, f2, f1);
+  const double f4 = __builtin_fma(nl, f3, 1.0);            // mul = 1.0 * f3 = f3
+  return __builtin_fma(f4, f3, f3);
+}
+__device__ __forceinline__ double sqrt_rt(double x) {
+#if RT_FAST_SQRT
+  if (wave_sqrt_core_ok(x)) return sqrt_core(x);
+#endif
+  return sqrt(x);
+}
+__device__ __forceinline__ double len(V3 a) { return sqrt_rt(dot(a, a)); }
+// l = len(a) and il = 1.0 / l, as `len(a)` and `1.0 / len(a)` compute them
+__device__ __forceinline__ void len_inv(V3 a, double* l, double* il) {
+  const double x = dot(a, a);
+#if RT_FAST_SQRT
+  if (wave_sqrt_core_ok(x)) {
+    *l = sqrt_core(x);
+    *il = recip_core(*l);
+    return;
+  }
+#endif
+  *l = sqrt(x);
+  *il = 1.0 / *l;
+}
+__device__ __forceinline__ V3 normalized(V3 a) {
+  double l, il;
+  len_inv(a, &l, &il);
+  return scale(a, il);
+}
 template <class P> __device__ __forceinline__ V3 ld3(P p) { return {p[0], p[1], p[2]}; }
 // transform_vector (transformation.rs:53-59) with rows m[0..3], m[4..7], m[8..11]
 template <class P> __device__ __forceinline__ V3 xf(P m, V3 v) {
@@ -244,7 +307,7 @@ __device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, boo
   if (sh && L->share_prev) {                                               // math_shapes.rs:42-62
     const double sum = sh->vd * sh->vd - (sh->vv - L->r2);
     if (sum < 0.0) return 0;
-    const double sq = sqrt(sum);
+    const double sq = sqrt_rt(sum);
     *t0 = (-sh->vd + sq) * sh->il;
     *t1 = (-sh->vd - sq) * sh->il;
     return 2;
@@ -264,14 +327,15 @@ __device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, boo
   int k = L->kind;
   if (k == RT_N_SPHERE) {                                                  // math_shapes.rs:42-62
     V3 v = sub(o, ld3(L->c));
-    double il = 1.0 / len(d);
+    double l, il;
+    len_inv(d, &l, &il);                                                   // il = 1.0 / len(d)
     V3 dn = scale(d, il);
     double vd = dot(v, dn);
     const double vv = dot(v, v);
     if (sh) *sh = {il, vd, vv};
     double sum = vd * vd - (vv - L->r2);
     if (sum < 0.0) return 0;
-    double sq = sqrt(sum);
+    double sq = sqrt_rt(sum);
     *t0 = (-vd + sq) * il;
     *t1 = (-vd - sq) * il;
     return 2;
@@ -782,8 +846,9 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
       for (int k = 0; k < S.n_lights; ++k) {
         cptr<RtLight> lt = &S.lights[k];
         const V3 lv = sub(ld3(lt->p), p);
-        const double ll = len(lv);
-        const V3 sdir = scale(lv, 1.0 / ll);                               // normalized(lv)
+        double ll, ill;
+        len_inv(lv, &ll, &ill);
+        const V3 sdir = scale(lv, ill);                                    // normalized(lv)
 #ifdef RT_ABLATE_NO_SHADOWS
         const double t = lv.x > 1e300 ? 0.5 : 1.0;
 #else
