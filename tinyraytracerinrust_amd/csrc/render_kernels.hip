@@ -26,6 +26,65 @@
 
 #define RT_HD __device__
 #include "rt_blob.h"
+// Correctly rounded sqrt(x) and 1/sqrt-derived reciprocals without their range handling.
+// For f64 `sqrt` and `/` the compiler emits (gfx950) scaled Newton sequences:
+//   sqrt(x): x scaled by 2^256 if x < 2^-767, y = rsq(x), g = x*y, h = 0.5*y, r = fma(-h,g,0.5),
+//            g = fma(g,r,g), h = fma(h,r,h), twice {d = fma(-g,g,x), g = fma(d,h,g)}, g scaled back,
+//            and x itself returned for +-0 / +inf (17 VALU instructions);
+//   a / b:   v_div_scale of b and of a, rcp, 4 Newton fmas, mul, fma, v_div_fmas, v_div_fixup (11).
+// For x in [2^-767, DBL_MAX] the scalings are by 2^0 and the class select returns g, so the
+// unscaled core below is the SAME operation sequence on the same values: bit-identical.  Then
+// l = sqrt(x) is in [2^-383.5, 2^512): for 1.0 / l v_div_scale scales neither operand (both
+// normal, exponent gap < 768, 1/l and the quotient normal), so v_div_fmas is a plain fma (VCC 0),
+// the mul by the numerator 1.0 is exact, and v_div_fixup returns its positive normal operand:
+// again the same values.  The range test is wave-uniform (one ballot), outside it the compiler's
+// sequences run.  RT_FAST_SQRT=0 restores the plain `sqrt` / `/` everywhere.
+#ifndef RT_FAST_SQRT
+#define RT_FAST_SQRT 1
+#endif
+static __device__ __forceinline__ double sqrt_core(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
+static __device__ __forceinline__ double recip_core(double l) {     // 1.0 / l for l in [2^-384, 2^512]
+  const double nl = -l;
+  const double r = __builtin_amdgcn_rcp(l);
+  const double f0 = __builtin_fma(nl, r, 1.0);
+  const double f1 = __builtin_fma(r, f0, r);
+  const double f2 = __builtin_fma(nl, f1, 1.0);
+  const double f3 = __builtin_fma(f1, f2, f1);
+  const double f4 = __builtin_fma(nl, f3, 1.0);            // mul = 1.0 * f3 = f3
+  return __builtin_fma(f4, f3, f3);
+}
+// a / b when neither v_div_scale scales (both operands normal, exponent gap < 768, quotient
+// normal, |a| >= 2^-969) or a == 0: the compiler's sequence with those identities dropped;
+// v_div_fixup is kept, so a zero numerator gives the same signed zero.
+static __device__ __forceinline__ double div_core(double a, double b) {
+  const double nb = -b;
+  const double r = __builtin_amdgcn_rcp(b);
+  const double f0 = __builtin_fma(nb, r, 1.0);
+  const double f1 = __builtin_fma(r, f0, r);
+  const double f2 = __builtin_fma(nb, f1, 1.0);
+  const double f3 = __builtin_fma(f1, f2, f1);
+  const double m = a * f3;
+  const double f4 = __builtin_fma(nb, m, a);
+  return __builtin_amdgcn_div_fixup(__builtin_fma(f4, f3, m), b, a);
+}
+// rt_math.h's rt_acos takes these for the operations whose operand ranges it guarantees.
+#ifndef RT_ACOS_CORES
+#define RT_ACOS_CORES 1
+#endif
+#if RT_FAST_SQRT && RT_ACOS_CORES
+#define RT_SQRT_IN_RANGE(x) sqrt_core(x)
+#define RT_DIV_IN_RANGE(a, b) div_core(a, b)
+#endif
 #include "rt_math.h"
 #include "scene.h"
 
@@ -117,45 +176,8 @@ __device__ __forceinline__ V3 add(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.
 __device__ __forceinline__ V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
 __device__ __forceinline__ V3 scale(V3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
 __device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-// Correctly rounded sqrt(x) and 1/sqrt-derived reciprocals without their range handling.
-// For f64 `sqrt` and `/` the compiler emits (gfx950) scaled Newton sequences:
-//   sqrt(x): x scaled by 2^256 if x < 2^-767, y = rsq(x), g = x*y, h = 0.5*y, r = fma(-h,g,0.5),
-//            g = fma(g,r,g), h = fma(h,r,h), twice {d = fma(-g,g,x), g = fma(d,h,g)}, g scaled back,
-//            and x itself returned for +-0 / +inf (17 VALU instructions);
-//   a / b:   v_div_scale of b and of a, rcp, 4 Newton fmas, mul, fma, v_div_fmas, v_div_fixup (11).
-// For x in [2^-767, DBL_MAX] the scalings are by 2^0 and the class select returns g, so the
-// unscaled core below is the SAME operation sequence on the same values: bit-identical.  Then
-// l = sqrt(x) is in [2^-383.5, 2^512): for 1.0 / l v_div_scale scales neither operand (both
-// normal, exponent gap < 768, 1/l and the quotient normal), so v_div_fmas is a plain fma (VCC 0),
-// the mul by the numerator 1.0 is exact, and v_div_fixup returns its positive normal operand:
-// again the same values.  The range test is wave-uniform (one ballot), outside it the compiler's
-// sequences run.  RT_FAST_SQRT=0 restores the plain `sqrt` / `/` everywhere.
-#ifndef RT_FAST_SQRT
-#define RT_FAST_SQRT 1
-#endif
 __device__ __forceinline__ bool wave_sqrt_core_ok(double x) {
   return __ballot(!(x >= 0x1p-767 && x <= 0x1.fffffffffffffp+1023)) == 0;
-}
-__device__ __forceinline__ double sqrt_core(double x) {
-  const double y = __builtin_amdgcn_rsq(x);
-  double g = x * y, h = y * 0.5;
-  const double r = __builtin_fma(-h, g, 0.5);
-  g = __builtin_fma(g, r, g);
-  h = __builtin_fma(h, r, h);
-  double d = __builtin_fma(-g, g, x);
-  g = __builtin_fma(d, h, g);
-  d = __builtin_fma(-g, g, x);
-  return __builtin_fma(d, h, g);
-}
-__device__ __forceinline__ double recip_core(double l) {     // 1.0 / l for l in [2^-384, 2^512]
-  const double nl = -l;
-  const double r = __builtin_amdgcn_rcp(l);
-  const double f0 = __builtin_fma(nl, r, 1.0);
-  const double f1 = __builtin_fma(r, f0, r);
-  const double f2 = __builtin_fma(nl, f1, 1.0);
-  const double f3 = __builtin_fma(f1, f2, f1);
-  const double f4 = __builtin_fma(nl, f3, 1.0);            // mul = 1.0 * f3 = f3
-  return __builtin_fma(f4, f3, f3);
 }
 __device__ __forceinline__ double sqrt_rt(double x) {
 #if RT_FAST_SQRT
@@ -673,7 +695,7 @@ __device__ __forceinline__ V3 refract_dir(V3 i, V3 n, double r, bool* tir) {   /
   double v = 1.0 - r * r * (1.0 - cos_1 * cos_1);
   *tir = v < 0.0;
   if (*tir) return {0.0, 0.0, 0.0};
-  double cos_2 = sqrt(v);
+  double cos_2 = sqrt_rt(v);
   return normalized(add(scale(i, r), scale(n, r * cos_1 - cos_2)));
 }
 

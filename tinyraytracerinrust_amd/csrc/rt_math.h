@@ -16,6 +16,17 @@
 #define RT_HD
 #endif
 
+// Operations whose operand ranges rt_acos guarantees (|x| < 1 branches): sqrt of z in
+// (2^-54, 1/4], p / q with p in (2^-120, 1) and q in [1/2, 1], and the residual quotient
+// fma(-s,s,z) / 2s (numerator 0 or |.| >= 2^-160).  The device build substitutes cores without the
+// scaling steps that are identities on those ranges (render_kernels.hip: bit-identical results).
+#ifndef RT_SQRT_IN_RANGE
+#define RT_SQRT_IN_RANGE(x) sqrt(x)
+#endif
+#ifndef RT_DIV_IN_RANGE
+#define RT_DIV_IN_RANGE(a, b) ((a) / (b))
+#endif
+
 RT_HD static inline double rt_asin_r(double z) {       // R(z) = P(z) / Q(z), asin(x) = x + x*R(x^2)
   const double pS0 = 1.66666666666666657415e-01, pS1 = -3.25565818622400915405e-01,
                pS2 = 2.01212532134862925881e-01, pS3 = -4.00555345006794114027e-02,
@@ -24,7 +35,7 @@ RT_HD static inline double rt_asin_r(double z) {       // R(z) = P(z) / Q(z), as
                qS3 = -6.88283971605453293030e-01, qS4 = 7.70381505559019352791e-02;
   double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
   double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-  return p / q;
+  return RT_DIV_IN_RANGE(p, q);
 }
 
 RT_HD static inline double rt_acos(double x) {
@@ -44,8 +55,8 @@ RT_HD static inline double rt_acos(double x) {
     return s + ((e + pio2_lo) - t);
   }
   const double z = (ax == x ? 1.0 - x : 1.0 + x) * 0.5;   // exact (Sterbenz)
-  const double s = sqrt(z);
-  const double sl = fma(-s, s, z) / (s + s);           // sqrt(z) = s + sl to ~2^-106
+  const double s = RT_SQRT_IN_RANGE(z);
+  const double sl = RT_DIV_IN_RANGE(fma(-s, s, z), s + s);           // sqrt(z) = s + sl to ~2^-106
   const double r = rt_asin_r(z);
   if (x > 0.0) {                                       // 2 asin(sqrt z)
     return 2.0 * (s + (sl + s * r));
