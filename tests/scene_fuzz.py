@@ -97,3 +97,39 @@ def random_scene(seed: int) -> str:
         lines.append(f"append light({_vec(r, -40, 40)}, {r.choice(_COLOURS)} * {_num(r, 0.3, 1)}, 100)")
     lines.append(f"set camera(<{_num(r, -20, 20)}, {_num(r, 0, 25)}, {_num(r, -110, -70)}>)")
     return "\n".join(lines) + "\n"
+
+
+def random_rod_scene(seed: int) -> str:
+    """Scenes built like globes.scene's axis rod and claw: a primitive scaled into a thin rod or
+    slab, intersected with (or cut from) another primitive, under nested rotate / translate blocks.
+    Their world boxes are loose, so the kernels' oriented object boxes (scene.cpp obb) cull these
+    objects in the leaf's own frame; the margins of that test meet grazing rays, rods seen end-on
+    and shadow rays along the rod here.  Opaque materials only (the reflection-only kernels take
+    the oriented boxes), reflective floors so secondary rays cross the rods too."""
+    r = random.Random(seed)
+    lines = [f"draw(plane(<0, 1, 0>, {_num(r, 20, 30)}, {_colour(r, False)}, {r.choice([0.2, 0.5])}))"]
+    for i in range(r.randint(2, 4)):
+        thin = [round(r.uniform(0.03, 0.15), 3), round(r.uniform(5, 100), 1), 1]
+        r.shuffle(thin)
+        lines.append(f"translate({_num(r, -15, 15)}, {_num(r, -8, 12)}, {_num(r, -10, 20)}) do")
+        lines.append(f"  rotate({_num(r, -3.1, 3.1)}, {_num(r, -3.1, 3.1)}, {_num(r, -3.1, 3.1)}) do")
+        lines.append(f"    scale({thin[0]}, {thin[1]}, {thin[2]}) do")
+        rod = f"sphere({_num(r, 0.5, 3)})" if r.random() < 0.5 else f"cube({_num(r, 1, 6)})"
+        lines.append(f"      a{i} = {rod}")
+        lines.append("    end")
+        other = f"cube({_num(r, 10, 40)})" if r.random() < 0.6 else f"sphere({_num(r, 8, 20)})"
+        op = r.choice(["intersection", "intersection", "difference"])
+        if op == "difference":                          # the rod is a: every hit lies inside it
+            lines.append(f"    s{i} = csg(a{i}, {other}, 'difference', {_material(r, False, allow_transp=False)})")
+        else:
+            lines.append(f"    s{i} = csg({other}, a{i}, 'intersection', {_material(r, False, allow_transp=False)})")
+        lines.append("  end")
+        lines.append("end")
+        lines.append(f"draw(s{i})")
+    if r.random() < 0.5:
+        lines.append(f"draw(sphere(<{_num(r, -10, 10)}, {_num(r, -5, 10)}, {_num(r, 0, 20)}>, {_num(r, 5, 12)}, "
+                     f"{_material(r, False, allow_transp=False)}))")
+    for _ in range(r.randint(0, 2)):
+        lines.append(f"append light({_vec(r, -40, 40)}, {r.choice(_COLOURS)} * {_num(r, 0.3, 1)}, 100)")
+    lines.append(f"set camera(<{_num(r, -20, 20)}, {_num(r, 0, 25)}, {_num(r, -110, -70)}>)")
+    return "\n".join(lines) + "\n"

@@ -8,7 +8,7 @@ exact, f64 colours within 1e-9 -- every case so far is bit-exact in RGBA8."""
 import numpy as np
 import pytest
 
-from tests.scene_fuzz import random_scene
+from tests.scene_fuzz import random_rod_scene, random_scene
 from tests.test_gpu_parity import assert_close
 
 pytestmark = pytest.mark.gpu
@@ -70,3 +70,35 @@ def test_random_scene_antialias(T, seed):
     assert grays == rrays
     assert np.abs(gf - rf).max() <= 1e-9
     assert np.array_equal(gu, ru), int((gu != ru).sum())
+
+
+@pytest.mark.parametrize("seed", range(3000, 3048))
+def test_rod_scene_small_frame(T, seed):
+    """Thin rotated rods and slabs (tests/scene_fuzz.py random_rod_scene): objects the kernels
+    cull with oriented boxes in a leaf's own frame (scene.cpp obb) -- exactness of that culling."""
+    from oracle import oracle as O
+    text = random_rod_scene(seed)
+    W, H, d = 128, 96, 8
+    rt = T.RayTracer(W, H)
+    rt.max_depth = d
+    rt.load_scene(text, 0.0)
+    gu = rt.renderer.render_rows_host(0, H)
+    gf = rt.renderer.render_rows_host(0, H, f64=True)
+    rf, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H, f64=True)
+    assert_close(gu, gf, ru, rf, f"rod scene {seed}")
+
+
+@pytest.mark.parametrize("seed", range(3100, 3106))
+def test_rod_scene_ordered_launches(T, seed):
+    """640x480: calibration, cost-ordered megakernel and (4800 tiles, tail-bound) deferred-shadow
+    launches over rod scenes: the oriented boxes in every traversal, shadow jobs included."""
+    from oracle import oracle as O
+    text = random_rod_scene(seed)
+    W, H, d = 640, 480, 10
+    rt = T.RayTracer(W, H)
+    rt.max_depth = d
+    rt.load_scene(text, 0.0)
+    frames = [rt.renderer.render_rows_host(0, H) for _ in range(3)]
+    _, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H)
+    for k, f in enumerate(frames):
+        assert_close(f, None, ru, None, f"rod scene {seed}, launch {k}")

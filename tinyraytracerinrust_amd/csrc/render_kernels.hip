@@ -480,6 +480,24 @@ template <class P> __device__ __forceinline__ bool box_may_hit(P lo, P hi, const
 }
 __device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) + 1e-7; }
 
+// The object's oriented box (RtObject::obb_leaf, scene.cpp obb): may the segment t in [0, tmax]
+// meet the leaf-frame box olo/ohi?  The ray is taken to the leaf's frame with the leaves' own
+// arithmetic; outside the range the host's margins are proven for (|o| <= 1e6, unit-length
+// directions) the answer is yes.  The refraction kernels (SHARE: 4 waves/SIMD at 115-119 VGPRs)
+// do not take it: the test's code alone made spinning_globes (no oriented box) 2.7 % slower
+// (profiles/r02cg_obb_ab.txt).
+#ifndef RT_OBB
+#define RT_OBB 1
+#endif
+__device__ __forceinline__ bool obb_may_hit(const DS& S, cptr<RtObject> O, V3 ro, V3 rd, double tmax) {
+  cptr<RtLeaf> R = &S.leaves[O->obb_leaf];
+  const double ad = fmax(fmax(fabs(rd.x), fabs(rd.y)), fabs(rd.z));
+  if (!(ad >= 0.25 && ad <= 4.0 && fabs(ro.x) <= 1e6 && fabs(ro.y) <= 1e6 && fabs(ro.z) <= 1e6)) return true;
+  const V3 o = xf(R->inv, ro);
+  const V3 d = sub(xf(R->inv, rd), ld3(R->inv_o));
+  return box_may_hit(O->olo, O->ohi, cull_ray(o, d), tmax);
+}
+
 // ------------------------------------------------------------------ traversal (raytracer.rs)
 // Both traversals walk the object hierarchy (RtTrav, pre-order over contiguous draw-order runs)
 // wave-coherently: `i` is uniform, a lane that misses a group resumes at its skip index, and the
@@ -518,6 +536,7 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
     if (O->cull == RT_CULL_ALWAYS) continue;
     if (O->cull == RT_CULL_BOX) CNT(cb + 1);
     if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, cr, cull_tmax(best))) continue;
+    if (RT_OBB && !SHARE && O->obb_leaf >= 0 && !obb_may_hit(S, O, ro, rd, cull_tmax(best))) continue;
     CNT(cb + 2);
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
     for (int l = lb; l < le; ++l) {
@@ -528,6 +547,7 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
         if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, cull_tmax(best))) continue;
       }
       CNT(cb + 4);
+      CNT(40 + cat * 8 + (o & 7));                      // per-object leaf evaluations (diagnostic)
       CNTW(35 + cat);
       CNT(cb + 5 + (L->kind == RT_N_SPHERE ? 0 : L->kind == RT_N_PLANE ? 1 : 2));
       double t0 = 0.0, t1 = 0.0;
@@ -576,6 +596,7 @@ __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
     if (O->shadow_skip || O->cull == RT_CULL_ALWAYS) continue;
     if (O->cull == RT_CULL_BOX) CNT(cb + 1);
     if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, cr, tmax)) continue;
+    if (RT_OBB && !SHARE && O->obb_leaf >= 0 && !obb_may_hit(S, O, p, dir, tmax)) continue;
     CNT(cb + 2);
     const double tobj = O->transparency;
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
@@ -587,6 +608,7 @@ __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
         if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
       }
       CNT(cb + 4);
+      CNT(56 + (T->obj & 7));
       CNTW(37);
       CNT(cb + 5 + (L->kind == RT_N_SPHERE ? 0 : L->kind == RT_N_PLANE ? 1 : 2));
       double t0 = 0.0, t1 = 0.0;

@@ -126,7 +126,10 @@ struct alignas(16) RtObject {
   double reflectivity, transparency;
   double blo[3], bhi[3];
   int32_t leaf_cull;                // 1: per-leaf boxes are tighter than the object box
-  int32_t pad2;
+  int32_t obb_leaf;                 // >= 0: every accepted hit of the object lies inside this leaf's
+                                    // region, whose box in the leaf's OWN frame (olo, ohi) is much
+                                    // tighter than blo/bhi (rotated thin rods and slabs); -1: none
+  double olo[3], ohi[3];            // that box in obb_leaf's object space, inflated (scene.cpp obb)
 };
 
 // Order-preserving object hierarchy: a pre-order list of nodes over CONTIGUOUS runs of objects

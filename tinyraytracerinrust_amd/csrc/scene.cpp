@@ -429,6 +429,71 @@ static void share_sphere_terms(FlatScene& f, RtObject* ob) {
   }
 }
 
+// ---------------------------------------------------------------- oriented object boxes
+// An object's accepted hits all lie inside leaf R's region when, for every leaf X of the object,
+// X is R or X's hit filter requires inside(R) (a literal 2R+1): a hit of R itself lies on R's
+// surface, any other accepted hit passed R's is_inside test.  R's region is a box in R's own
+// frame (sphere: centre +- (r + EPS), cube: [lo, hi]), so a ray whose image under R's inverse
+// transform misses that box cannot produce an accepted hit of the object.  The kernels test it
+// after the world box (render_kernels.hip obb_may_hit) when its world volume is under half the
+// world box's -- e.g. globes.scene's tilted axis rod and thin claw slab.
+//
+// Margins (local units, per axis i, on top of the box): the kernel forms o' = xf(inv, o) and
+// d' = xf(inv, d) - inv_o exactly as the leaves do, so R's own hits are at the same o' + t d';
+// other leaves' hits were tested at q = xf(inv, p), p = o + t d.  Their difference is rounding:
+// <= ~4 ulp of (|M_i| |p| + |T_i|) for q, the same for o', and t times ~2 ulp of
+// (|M_i| |d| + |T_i|) for d' (the - inv_o cancels T).  The kernel only takes the test for
+// |o| <= 1e6 and |d|_max in [1/4, 4] (unit-length directions), and |p| <= 1e6 inside the world
+// box, so t <= 8e6 and the error is < 1e-8 (|M_i| + |T_i|); the margin is 1e-6 (1 + |M_i| + |T_i|)
+// plus 1e-6 of the box coordinates, and the slab arithmetic itself is the world box test's
+// (cull_ray / box_may_hit).
+static void obb(FlatScene& f, RtObject* ob) {
+  ob->obb_leaf = -1;
+  if (ob->cull != RT_CULL_BOX || getenv("RT_NO_OBB")) return;
+  double wvol = 1.0;
+  for (int i = 0; i < 3; ++i) wvol *= ob->bhi[i] - ob->blo[i];
+  double best = 0.5 * wvol;
+  for (int32_t r = ob->leaf_begin; r < ob->leaf_begin + ob->leaf_count; ++r) {
+    const RtLeaf& R = f.leaves[r];
+    if (R.kind != RT_N_SPHERE && R.kind != RT_N_CUBE) continue;
+    bool all = true;
+    for (int32_t x = ob->leaf_begin; x < ob->leaf_begin + ob->leaf_count && all; ++x) {
+      if (x == r) continue;
+      const RtLeaf& X = f.leaves[x];
+      bool req = false;
+      for (int k = 0; k < X.n_lit && !req; ++k) req = X.lit[k] == 2 * r + 1;
+      all = req;                       // n_lit < 0 (a disjunctive filter): never required
+    }
+    if (!all) continue;
+    double lo[3], hi[3];
+    for (int i = 0; i < 3; ++i) {
+      lo[i] = R.kind == RT_N_SPHERE ? R.c[i] - R.r_eps : R.lo[i];
+      hi[i] = R.kind == RT_N_SPHERE ? R.c[i] + R.r_eps : R.hi[i];
+    }
+    const double* M = R.inv;
+    const double det = M[0] * (M[5] * M[10] - M[6] * M[9]) - M[1] * (M[4] * M[10] - M[6] * M[8]) +
+                       M[2] * (M[4] * M[9] - M[5] * M[8]);
+    if (!std::isfinite(det) || !(fabs(det) > 1e-300)) continue;
+    bool ok = true;
+    double vol = 1.0;
+    for (int i = 0; i < 3 && ok; ++i) {
+      const double mi = fabs(M[4 * i]) + fabs(M[4 * i + 1]) + fabs(M[4 * i + 2]), ti = fabs(M[4 * i + 3]) + fabs(R.inv_o[i]);
+      const double m = 1e-6 * (1.0 + mi + ti) + 1e-6 * (fabs(lo[i]) + fabs(hi[i]));
+      lo[i] -= m;
+      hi[i] += m;
+      ok = std::isfinite(lo[i]) && std::isfinite(hi[i]) && fabs(lo[i]) <= RT_CULL_COORD_MAX && fabs(hi[i]) <= RT_CULL_COORD_MAX;
+      vol *= hi[i] - lo[i];
+    }
+    if (!ok) continue;
+    vol /= fabs(det);                  // world volume of the local box
+    if (vol < best) {
+      best = vol;
+      ob->obb_leaf = r;
+      for (int i = 0; i < 3; ++i) { ob->olo[i] = lo[i]; ob->ohi[i] = hi[i]; }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- object hierarchy
 static double box_area(const double* lo, const double* hi) {
   const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
@@ -565,6 +630,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
         ++n_leaf_boxes_tighter;
     }
     ob.leaf_cull = n_leaf_boxes_tighter > 0;
+    obb(f, &ob);
     const rt_material& m = o.mat;
     ob.textured = m.texture >= 0;
     ob.tex = m.texture >= 0 ? m.texture : 0;
@@ -602,8 +668,9 @@ int flatten(const rt_scene& s, FlatScene* out) {
               f.trav[i].blo[0], f.trav[i].blo[1], f.trav[i].blo[2], f.trav[i].bhi[0], f.trav[i].bhi[1], f.trav[i].bhi[2]);
     for (size_t o = 0; o < f.objects.size(); ++o) {
       const RtObject& ob = f.objects[o];
-      fprintf(stderr, "object %zu cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] leaves %d leaf_cull=%d\n", o, ob.cull,
-              ob.blo[0], ob.blo[1], ob.blo[2], ob.bhi[0], ob.bhi[1], ob.bhi[2], ob.leaf_count, ob.leaf_cull);
+      fprintf(stderr, "object %zu cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] leaves %d leaf_cull=%d obb_leaf=%d "
+              "[%.3f %.3f %.3f]..[%.3f %.3f %.3f]\n", o, ob.cull, ob.blo[0], ob.blo[1], ob.blo[2], ob.bhi[0], ob.bhi[1],
+              ob.bhi[2], ob.leaf_count, ob.leaf_cull, ob.obb_leaf, ob.olo[0], ob.olo[1], ob.olo[2], ob.ohi[0], ob.ohi[1], ob.ohi[2]);
       for (int l = ob.leaf_begin; l < ob.leaf_begin + ob.leaf_count; ++l) {
         const RtLeaf& L = f.leaves[l];
         fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d lits %d xdiag %d share %d axis %d\n", l, L.kind,

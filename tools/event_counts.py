@@ -47,3 +47,7 @@ for W, H, d in [(W0, H0, dd) for dd in DEPTHS]:
         wc, wl = buf[32 + c], buf[35 + c]
         print(f"  {nm:9s} traversal calls: {buf[c * 9] / max(1, 64 * wc):.3f} of lanes active; "
               f"leaf evaluations: {buf[c * 9 + 4] / max(1, 64 * wl):.3f} of lanes active ({wc} wave calls, {wl} wave leaf evals)")
+    # per-object leaf evaluations (lane-events; objects in draw order, index mod 8)
+    for c, nm in enumerate(["primary", "secondary", "shadow"]):
+        print(f"  {nm:9s} leaf evals by object: " + " ".join(f"{o}:{buf[40 + c * 8 + o]}" for o in range(8)))
+
