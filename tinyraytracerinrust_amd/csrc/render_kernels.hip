@@ -161,6 +161,10 @@ constexpr double EPS = RT_EPSILON;
 #ifndef RT_PLANE_AXIS
 #define RT_PLANE_AXIS 1             // axis-aligned planes: one product per dot in the traversals
 #endif
+#ifndef RT_SHARE_MEGA
+#define RT_SHARE_MEGA 0             // 1: shared sphere terms in the reflection-only kernels too: 7-8 % slower
+                                    // (20 spilled VGPRs, profiles/r02cm_share_mega_ab.txt)
+#endif
 #ifndef RT_SPHERE_SHARE
 #define RT_SPHERE_SHARE 1           // concentric sphere leaves with one transform share their ray terms
 #endif
@@ -508,7 +512,7 @@ __device__ __forceinline__ bool obb_may_hit(const DS& S, cptr<RtObject> O, V3 ro
 // filter: candidates that cannot win never pay for the sibling is_inside tests.
 // SHARE: concentric sphere leaves reuse their ray terms (SphereShare); it keeps three doubles live
 // across the leaf loop, so only kernels with register headroom take it (see trace()).
-template <bool SHARE = false>
+template <bool SHARE = false, bool OBB = !SHARE>
 __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0) {
   [[maybe_unused]] const int cb = cat * 9;
   CNT(cb + 0);
@@ -536,7 +540,7 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
     if (O->cull == RT_CULL_ALWAYS) continue;
     if (O->cull == RT_CULL_BOX) CNT(cb + 1);
     if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, cr, cull_tmax(best))) continue;
-    if (RT_OBB && !SHARE && O->obb_leaf >= 0 && !obb_may_hit(S, O, ro, rd, cull_tmax(best))) continue;
+    if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, ro, rd, cull_tmax(best))) continue;
     CNT(cb + 2);
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
     for (int l = lb; l < le; ++l) {
@@ -569,7 +573,7 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
 // Product of the transparencies of every filtered hit with EPS < d < dist (raytracer.rs:181-197).
 // Early-out once the product is exactly 0 (it stays 0: every factor is finite, checked on the
 // host), objects of transparency exactly 1.0 are skipped (x * 1.0 == x).
-template <bool SHARE = false>
+template <bool SHARE = false, bool OBB = !SHARE>
 __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
   [[maybe_unused]] constexpr int cb = 18;
   CNT(cb + 0);
@@ -596,7 +600,7 @@ __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
     if (O->shadow_skip || O->cull == RT_CULL_ALWAYS) continue;
     if (O->cull == RT_CULL_BOX) CNT(cb + 1);
     if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, cr, tmax)) continue;
-    if (RT_OBB && !SHARE && O->obb_leaf >= 0 && !obb_may_hit(S, O, p, dir, tmax)) continue;
+    if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, p, dir, tmax)) continue;
     CNT(cb + 2);
     const double tobj = O->transparency;
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
@@ -854,7 +858,8 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
   // the registers (104 -> 116 VGPRs, no spill; spinning_globes 1080p 4.8 % faster), while the
   // reflection-only megakernel at 5 waves spills 14 more VGPRs and runs 6 % slower on 4K globes
   // (profiles/r02am_ab.txt).
-  constexpr bool SHARE = REFR && RT_SPHERE_SHARE;
+  constexpr bool SHARE = (REFR || RT_SHARE_MEGA) && RT_SPHERE_SHARE;
+  constexpr bool OBB = !REFR;                          // oriented object boxes: reflection-only kernels
   int fSlot[RECORD ? RT_MAX_DEPTH_CAP : 1];
   [[maybe_unused]] int ray_type = 0, slot = 0;                  // RayType::NormalRay
   int sp = 0, depth = 0;
@@ -864,7 +869,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
     bool descend = false;
     double t_hit;
     PROF_T0(p0);
-    const int oi = nearest_hit<SHARE>(S, ro, rd, &t_hit, trip == 0 ? 0 : 1);
+    const int oi = nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit, trip == 0 ? 0 : 1);
     PROF_ADD(trip == 0 ? 0 : 1, p0);
     ++trip;
     PROF_T0(p1);
@@ -897,7 +902,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
         const double t = lv.x > 1e300 ? 0.5 : 1.0;
 #else
         PROF_T0(p2);
-        const double t = shadow_transparency<SHARE>(S, p, sdir, ll);       // :176-197
+        const double t = shadow_transparency<SHARE, OBB>(S, p, sdir, ll);       // :176-197
         PROF_ADD(2, p2);
 #endif
         if (!have_shading) {
@@ -927,7 +932,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
           const double t = lv.x > 1e300 ? 0.5 : 1.0;
 #else
           PROF_T0(p2);
-          const double t = shadow_transparency<SHARE>(S, p, normalized(lv), len(lv));   // :176-197
+          const double t = shadow_transparency<SHARE, OBB>(S, p, normalized(lv), len(lv));   // :176-197
           PROF_ADD(2, p2);
 #endif
 #pragma unroll
