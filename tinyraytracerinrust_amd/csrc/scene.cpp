@@ -429,6 +429,49 @@ static void share_sphere_terms(FlatScene& f, RtObject* ob) {
   }
 }
 
+// ---------------------------------------------------------------- hit-filter literal order
+// A literal filter is a conjunction of pure tests, so its order is free (the kernels stop at the
+// first failing literal).  Most likely failures first: for a hit of leaf X, "inside R" fails about
+// 1 - vol(R)/vol(X) of the time and "not inside R" about vol(R)/vol(X) (world volumes of the
+// leaves' regions); for spheres sharing X's transform and centre the answer is known from the radii
+// (globes.scene's claw: a hit on the outer shell is never inside the inner one, but is usually
+// outside the thin slab, so the slab test goes first).
+static double leaf_world_volume(const RtLeaf& L) {
+  const double* M = L.inv;
+  const double det = M[0] * (M[5] * M[10] - M[6] * M[9]) - M[1] * (M[4] * M[10] - M[6] * M[8]) +
+                     M[2] * (M[4] * M[9] - M[5] * M[8]);
+  const double v = L.kind == RT_N_SPHERE ? 4.18879020478639 * L.radius * L.radius * L.radius
+                 : L.kind == RT_N_CUBE ? 8.0 * L.radius * L.radius * L.radius : INFINITY;
+  return std::isfinite(det) && det != 0.0 ? fabs(v / det) : INFINITY;
+}
+
+static void order_literals(FlatScene& f, const RtObject& ob) {
+  for (int32_t x = ob.leaf_begin; x < ob.leaf_begin + ob.leaf_count; ++x) {
+    RtLeaf& X = f.leaves[x];
+    if (X.n_lit < 2) continue;
+    const double vx = leaf_world_volume(X);
+    double fail[RT_MAX_LITS];
+    for (int k = 0; k < X.n_lit; ++k) {
+      const RtLeaf& R = f.leaves[X.lit[k] >> 1];
+      const bool want = X.lit[k] & 1;
+      if (X.kind == RT_N_SPHERE && R.kind == RT_N_SPHERE && shares_sphere_terms(X, R)) {
+        fail[k] = want ? (X.radius < R.radius ? 0.0 : 1.0) : (X.radius > R.radius ? 0.0 : 1.0);
+        continue;
+      }
+      const double vr = leaf_world_volume(R);
+      const double frac = std::isfinite(vx) && std::isfinite(vr) && vx > 0.0 ? std::min(1.0, vr / vx) : 0.5;
+      fail[k] = want ? 1.0 - frac : frac;
+    }
+    int idx[RT_MAX_LITS];
+    for (int k = 0; k < X.n_lit; ++k) idx[k] = k;
+    std::stable_sort(idx, idx + X.n_lit, [&](int a, int b) { return fail[a] > fail[b]; });
+    int32_t lits[RT_MAX_LITS];
+    for (int k = 0; k < X.n_lit; ++k) lits[k] = X.lit[idx[k]];
+    if (!getenv("RT_NO_LIT_ORDER"))
+      for (int k = 0; k < X.n_lit; ++k) X.lit[k] = lits[k];
+  }
+}
+
 // ---------------------------------------------------------------- oriented object boxes
 // An object's accepted hits all lie inside leaf R's region when, for every leaf X of the object,
 // X is R or X's hit filter requires inside(R) (a literal 2R+1): a hit of R itself lies on R's
@@ -631,6 +674,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
     }
     ob.leaf_cull = n_leaf_boxes_tighter > 0;
     obb(f, &ob);
+    order_literals(f, ob);
     const rt_material& m = o.mat;
     ob.textured = m.texture >= 0;
     ob.tex = m.texture >= 0 ? m.texture : 0;
@@ -673,9 +717,10 @@ int flatten(const rt_scene& s, FlatScene* out) {
               ob.bhi[2], ob.leaf_count, ob.leaf_cull, ob.obb_leaf, ob.olo[0], ob.olo[1], ob.olo[2], ob.ohi[0], ob.ohi[1], ob.ohi[2]);
       for (int l = ob.leaf_begin; l < ob.leaf_begin + ob.leaf_count; ++l) {
         const RtLeaf& L = f.leaves[l];
-        fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d lits %d xdiag %d share %d axis %d\n", l, L.kind,
+        fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d lits %d (%d %d %d) xdiag %d share %d axis %d\n", l, L.kind,
                 L.cull, L.blo[0], L.blo[1], L.blo[2], L.bhi[0], L.bhi[1], L.bhi[2], L.prog_end - L.prog_begin, L.n_lit,
-                L.xdiag, L.share_prev, L.plane_axis);
+                L.n_lit > 0 ? L.lit[0] : -1, L.n_lit > 1 ? L.lit[1] : -1, L.n_lit > 2 ? L.lit[2] : -1, L.xdiag, L.share_prev,
+                L.plane_axis);
       }
     }
   }

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--burst", type=int, default=1,
                     help="launches back to back per measurement (sustained clocks); the time per launch is "
                          "the burst's wall time / burst")
+    ap.add_argument("--upload-env", nargs="*", default=[],
+                    help="per library (in order): KEY=VAL set in the environment while its scene is compiled and "
+                         "uploaded (host-side flattening switches, e.g. RT_NO_LIT_ORDER=1); '-' for none")
     a = ap.parse_args()
     import torch
     W, H = (int(v) for v in a.size.split("x"))
@@ -34,13 +37,19 @@ def main():
     out = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     ctxs = []
-    for path in a.libs:
+    for li, path in enumerate(a.libs):
+        env = a.upload_env[li] if li < len(a.upload_env) and a.upload_env[li] != "-" else None
+        if env:
+            k, v = env.split("=", 1)
+            os.environ[k] = v
         L = ctypes.CDLL(os.path.abspath(path))
         sc, cx = ctypes.c_void_p(), ctypes.c_void_p()
         assert L.rt_scene_compile(text, SCENES.encode(), ctypes.c_double(a.time), W, H, ctypes.byref(sc)) == 0
         assert L.rt_ctx_create(0, ctypes.byref(cx)) == 0
         assert L.rt_ctx_upload(cx, sc) == 0
-        ctxs.append((path, L, cx, []))
+        if env:
+            del os.environ[env.split("=", 1)[0]]
+        ctxs.append((path + (f" [{env}]" if env else ""), L, cx, []))
     import time
     for rep in range(a.reps + 3):
         for path, L, cx, ms in ctxs:
