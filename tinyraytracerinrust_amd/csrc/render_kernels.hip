@@ -161,6 +161,12 @@ constexpr double EPS = RT_EPSILON;
 #ifndef RT_PLANE_AXIS
 #define RT_PLANE_AXIS 1             // axis-aligned planes: one product per dot in the traversals
 #endif
+#ifndef RT_CONST_FILTER
+#define RT_CONST_FILTER 1           // skip hit filters the host proved constant (RtLeaf::filter_const) in the
+                                    // refraction kernels (SHARE): spinning_globes' glass shells, 10.5 % faster;
+                                    // in the reflection-only megakernel the test cost 4 more spilled VGPRs
+                                    // (profiles/r02co_const_filter_ab.txt)
+#endif
 #ifndef RT_SHARE_MEGA
 #define RT_SHARE_MEGA 0             // 1: shared sphere terms in the reflection-only kernels too: 7-8 % slower
                                     // (20 spilled VGPRs, profiles/r02cm_share_mega_ab.txt)
@@ -556,7 +562,7 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
       CNT(cb + 5 + (L->kind == RT_N_SPHERE ? 0 : L->kind == RT_N_PLANE ? 1 : 2));
       double t0 = 0.0, t1 = 0.0;
       int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1, SHARE ? &shr : nullptr);
-      const bool filtered = L->prog_end != L->prog_begin;
+      const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && SHARE && L->filter_const && !isnan(cr.inv.x));
       if (filtered && ((n >= 1 && t0 > EPS && t0 < best) || (n >= 2 && t1 > EPS))) CNT(cb + 8);
       if (n >= 1 && t0 > EPS && t0 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) {
         best = t0; bobj = o;
@@ -617,7 +623,7 @@ __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
       CNT(cb + 5 + (L->kind == RT_N_SPHERE ? 0 : L->kind == RT_N_PLANE ? 1 : 2));
       double t0 = 0.0, t1 = 0.0;
       int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1, SHARE ? &shr : nullptr);
-      const bool filtered = L->prog_end != L->prog_begin;
+      const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && SHARE && L->filter_const && !isnan(cr.inv.x));
       if (filtered && ((n >= 1 && t0 > EPS && t0 < dist) || (n >= 2 && t1 > EPS && t1 < dist))) CNT(cb + 8);
       if (n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) {
         tr *= tobj;

@@ -77,6 +77,9 @@ struct alignas(16) RtLeaf {
   int32_t n_lit;        // >= 0: the filter program is the conjunction of n_lit literals below
   int32_t lit[RT_MAX_LITS];   // literal = 2 * leaf + want: leaf[lit >> 1].is_inside(p) == (lit & 1)
   int32_t plane_axis;   // untransformed plane leaf: 0/1/2 when pnorm has exactly one nonzero (finite) component; else -1
+  int32_t filter_const; // 1: every literal of the hit filter passes for any hit of this leaf whose ray origin is
+                        // within 1e6 (concentric spheres under one transform, radii apart by more than the
+                        // rounding margin: scene.cpp const_filters), so the traversals skip the filter
   int32_t share_prev;   // sphere leaf: 1 = the previous leaf of the object is a sphere with a bit-identical
                         // inverse transform (inv, inv_o, xdiag) and centre, and every traversal that
                         // evaluates this leaf has evaluated that one first (see below)

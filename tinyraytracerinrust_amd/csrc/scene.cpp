@@ -472,6 +472,40 @@ static void order_literals(FlatScene& f, const RtObject& ob) {
   }
 }
 
+// ---------------------------------------------------------------- constant hit filters
+// A hit of sphere X tested against a sphere R with the same transform and centre (bit-identical
+// inv, inv_o, c): the filter's point q = xf(inv, o + t d) lies at |q - c| = r_X up to rounding in
+// the quadratic's t, the world point and the transform, all below ~1e-14 (1 + |M|) (|o| + |p| +
+// |T| + |c| + r) -- |p| is bounded by the sphere's world extent, and the traversals only skip the
+// filter for ray origins |o| <= 1e6 (their culling ray's range, render_kernels.hip cull_ray).  With
+// the margin m below (>= 1e6 x that bound) "inside R" (|q - c| <= r_R + EPS) is always true when
+// r_X + m < r_R and always false when r_X - m > r_R + EPS: spinning_globes.scene's glass shells,
+// globes.scene's claw.  A filter whose every literal always passes is skipped (filter_const).
+static void const_filters(FlatScene& f, const RtObject& ob) {
+  for (int32_t x = ob.leaf_begin; x < ob.leaf_begin + ob.leaf_count; ++x) {
+    RtLeaf& X = f.leaves[x];
+    X.filter_const = 0;
+    if (X.kind != RT_N_SPHERE || X.n_lit < 1 || getenv("RT_NO_CONST_FILTER")) continue;
+    double mrow = 0.0, fwd = 0.0, tsum = 0.0;
+    for (int i = 0; i < 3; ++i) {
+      mrow = std::max(mrow, fabs(X.inv[4 * i]) + fabs(X.inv[4 * i + 1]) + fabs(X.inv[4 * i + 2]));
+      fwd = std::max(fwd, fabs(X.mat[4 * i]) + fabs(X.mat[4 * i + 1]) + fabs(X.mat[4 * i + 2]));
+      tsum += fabs(X.inv[4 * i + 3]) + fabs(X.inv_o[i]) + fabs(X.mat[4 * i + 3]) + fabs(X.c[i]);
+    }
+    bool all = true;
+    for (int k = 0; k < X.n_lit && all; ++k) {
+      const RtLeaf& R = f.leaves[X.lit[k] >> 1];
+      const bool want = X.lit[k] & 1;
+      if (R.kind != RT_N_SPHERE || !shares_sphere_terms(X, R)) { all = false; break; }
+      const double extent = fwd * (tsum + X.radius + R.radius) + tsum;     // bounds |p| for hits of X
+      const double m = 1e-8 * (1.0 + mrow) * (1e6 + extent + tsum + X.radius + R.radius);
+      const bool finite = std::isfinite(m) && std::isfinite(X.radius) && std::isfinite(R.r_eps);
+      all = finite && (want ? X.radius + m < R.radius : X.radius - m > R.r_eps);
+    }
+    X.filter_const = all ? 1 : 0;
+  }
+}
+
 // ---------------------------------------------------------------- oriented object boxes
 // An object's accepted hits all lie inside leaf R's region when, for every leaf X of the object,
 // X is R or X's hit filter requires inside(R) (a literal 2R+1): a hit of R itself lies on R's
@@ -675,6 +709,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
     ob.leaf_cull = n_leaf_boxes_tighter > 0;
     obb(f, &ob);
     order_literals(f, ob);
+    const_filters(f, ob);
     const rt_material& m = o.mat;
     ob.textured = m.texture >= 0;
     ob.tex = m.texture >= 0 ? m.texture : 0;
@@ -717,9 +752,9 @@ int flatten(const rt_scene& s, FlatScene* out) {
               ob.bhi[2], ob.leaf_count, ob.leaf_cull, ob.obb_leaf, ob.olo[0], ob.olo[1], ob.olo[2], ob.ohi[0], ob.ohi[1], ob.ohi[2]);
       for (int l = ob.leaf_begin; l < ob.leaf_begin + ob.leaf_count; ++l) {
         const RtLeaf& L = f.leaves[l];
-        fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d lits %d (%d %d %d) xdiag %d share %d axis %d\n", l, L.kind,
+        fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d lits %d (%d %d %d) const %d xdiag %d share %d axis %d\n", l, L.kind,
                 L.cull, L.blo[0], L.blo[1], L.blo[2], L.bhi[0], L.bhi[1], L.bhi[2], L.prog_end - L.prog_begin, L.n_lit,
-                L.n_lit > 0 ? L.lit[0] : -1, L.n_lit > 1 ? L.lit[1] : -1, L.n_lit > 2 ? L.lit[2] : -1, L.xdiag, L.share_prev,
+                L.n_lit > 0 ? L.lit[0] : -1, L.n_lit > 1 ? L.lit[1] : -1, L.n_lit > 2 ? L.lit[2] : -1, L.filter_const, L.xdiag, L.share_prev,
                 L.plane_axis);
       }
     }
