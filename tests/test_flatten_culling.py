@@ -1,0 +1,82 @@
+"""Host-side culling facts the kernels rely on (tinyraytracerinrust_amd/csrc/scene.cpp), read from
+the flattener's RT_DUMP_FLAT report: oriented object boxes (obb), the order of hit-filter
+literals (order_literals) and constant hit filters (const_filters).  Each is exact by construction
+(DESIGN.md §2); the pixels are compared with the oracle on the GPU (tests/test_gpu_*.py)."""
+import os
+import re
+import subprocess
+import sys
+
+from tests.conftest import ROOT
+
+SCENES = os.path.join(ROOT, "tests", "golden", "scenes")
+
+
+def _dump(scene_text: str, time: float = 0.0) -> str:
+    code = ("import ctypes, sys; sys.path.insert(0, '.'); import tinyraytracerinrust_amd as T; "
+            "s = T.Scene.compile(sys.stdin.read(), %r, 64, 48, asset_dir=%r); "
+            "n = ctypes.c_int32(); sys.exit(T.lib().rt_scene_traversal(s.h, None, None, 0, ctypes.byref(n)))"
+            % (time, SCENES))
+    p = subprocess.run([sys.executable, "-c", code], input=scene_text, capture_output=True, text=True, cwd=ROOT,
+                       env=dict(os.environ, RT_DUMP_FLAT="1"), timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    return p.stderr
+
+
+def _objects(dump: str):
+    objs = []
+    for line in dump.splitlines():
+        m = re.match(r"object (\d+) .* obb_leaf=(-?\d+)", line)
+        if m:
+            objs.append({"obb": int(m.group(2)), "leaves": []})
+        m = re.match(r"\s+leaf (\d+) kind=(\d+) .* lits (-?\d+) \((-?\d+) (-?\d+) (-?\d+)\) const (\d)", line)
+        if m:
+            n = int(m.group(3))
+            objs[-1]["leaves"].append({"leaf": int(m.group(1)), "kind": int(m.group(2)),
+                                       "lits": [int(m.group(4 + k)) for k in range(max(0, min(n, 3)))],
+                                       "const": int(m.group(7))})
+    return objs
+
+
+def test_globes_oriented_boxes_and_literal_order():
+    objs = _objects(_dump(open(os.path.join(SCENES, "globes.scene")).read()))
+    assert len(objs) == 6
+    # plane, base, support, globe: the world box is tight enough; claw and axis rod: a leaf's frame
+    assert [o["obb"] >= 0 for o in objs] == [False, False, False, True, False, True]
+    claw = objs[3]["leaves"]
+    s20, s18, cube = (l["leaf"] for l in claw)
+    assert objs[3]["obb"] == cube                               # the thin slab, not the 40-wide sphere
+    # a hit on either shell: the slab test (usually failing) before the shell test (never failing)
+    assert claw[0]["lits"] == [2 * cube + 1, 2 * s18 + 0]
+    assert claw[1]["lits"] == [2 * cube + 1, 2 * s20 + 1]
+    # a hit on the slab face: "not inside the inner sphere" fails more often than "inside the outer"
+    assert claw[2]["lits"] == [2 * s18 + 0, 2 * s20 + 1]
+    # the claw's filters also test the slab: not constant
+    assert not any(l["const"] for o in objs for l in o["leaves"])
+
+
+def test_spinning_globes_shell_filters_are_constant():
+    objs = _objects(_dump(open(os.path.join(SCENES, "spinning_globes.scene")).read(), 0.3))
+    shells = [o for o in objs if len(o["leaves"]) == 2]
+    assert len(shells) == 3
+    for o in shells:
+        assert [l["const"] for l in o["leaves"]] == [1, 1]
+
+
+def test_constant_filter_needs_a_radius_gap_and_one_transform():
+    # a shell 0.5 thick at radius 10: above the margin (~0.02 for origins within 1e6) -> constant
+    thick = "draw(csg(sphere(<0, 0, 0>, 10), sphere(<0, 0, 0>, 9.5), 'difference', red, 0, 0.5))\n"
+    assert [l["const"] for l in _objects(_dump(thick))[0]["leaves"]] == [1, 1]
+    # 1e-3 thick: inside the margin -> evaluated
+    thin = "draw(csg(sphere(<0, 0, 0>, 10), sphere(<0, 0, 0>, 9.999), 'difference', red, 0, 0.5))\n"
+    assert [l["const"] for l in _objects(_dump(thin))[0]["leaves"]] == [0, 0]
+    # the same radii: no gap -> evaluated
+    same = "draw(csg(sphere(<0, 0, 0>, 10), sphere(<0, 0, 0>, 10), 'difference', red, 0, 0.5))\n"
+    assert [l["const"] for l in _objects(_dump(same))[0]["leaves"]] == [0, 0]
+    # different centres -> evaluated
+    off = "draw(csg(sphere(<0, 0, 0>, 10), sphere(<1, 0, 0>, 5), 'difference', red, 0, 0.5))\n"
+    assert [l["const"] for l in _objects(_dump(off))[0]["leaves"]] == [0, 0]
+    # the inner sphere under a further transform -> evaluated
+    xf = ("a = sphere(<0, 0, 0>, 10)\nscale(1, 2, 1) do\n  b = sphere(<0, 0, 0>, 5)\nend\n"
+          "draw(csg(a, b, 'difference', red, 0, 0.5))\n")
+    assert [l["const"] for l in _objects(_dump(xf))[0]["leaves"]] == [0, 0]
