@@ -80,3 +80,14 @@ def test_constant_filter_needs_a_radius_gap_and_one_transform():
     xf = ("a = sphere(<0, 0, 0>, 10)\nscale(1, 2, 1) do\n  b = sphere(<0, 0, 0>, 5)\nend\n"
           "draw(csg(a, b, 'difference', red, 0, 0.5))\n")
     assert [l["const"] for l in _objects(_dump(xf))[0]["leaves"]] == [0, 0]
+
+
+def test_shadow_walk_visits_likeliest_occluders_first():
+    """globes.scene has no transparent object: shadow rays only ask whether any object occludes,
+    so their walk (strav) takes the largest regions first -- the globe, the claw slab, the base,
+    the axis rod, the support rod -- and the unbounded floor plane last.  spinning_globes.scene
+    (glass shells) keeps the draw order: its shadow product's order is the reference's."""
+    def strav(dump):
+        return [int(m.group(1)) for m in re.finditer(r"^strav \d+ obj=(-?\d+)", dump, re.M) if int(m.group(1)) >= 0]
+    assert strav(_dump(open(os.path.join(SCENES, "globes.scene")).read())) == [4, 3, 1, 5, 2, 0]
+    assert strav(_dump(open(os.path.join(SCENES, "spinning_globes.scene")).read(), 0.3)) == [0, 1, 2, 3]

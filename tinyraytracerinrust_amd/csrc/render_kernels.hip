@@ -142,13 +142,14 @@ template <class T> __device__ __forceinline__ cptr<T> as_const(const T* p) { ret
 struct DS {                         // device view of RtDevScene
   cptr<RtObject> objects;
   cptr<RtTrav> trav;
+  cptr<RtTrav> strav;               // shadow-ray walk of scenes without a transparent object
   cptr<RtNode> nodes;
   cptr<RtLeaf> leaves;
   cptr<RtProg> prog;
   cptr<RtLight> lights;
   cptr<RtTexture> textures;
   const uint8_t* texels;            // per-lane texel gathers stay global (vector) loads
-  int n_objects, n_lights, n_trav;
+  int n_objects, n_lights, n_trav, n_strav;
   int shadow_early_out;
 };
 
@@ -160,6 +161,9 @@ constexpr double EPS = RT_EPSILON;
 #endif
 #ifndef RT_PLANE_AXIS
 #define RT_PLANE_AXIS 1             // axis-aligned planes: one product per dot in the traversals
+#endif
+#ifndef RT_SHADOW_ORDER
+#define RT_SHADOW_ORDER 1           // reflection-only kernels: shadow rays walk the likeliest occluders first
 #endif
 #ifndef RT_CONST_FILTER
 #define RT_CONST_FILTER 1           // skip hit filters the host proved constant (RtLeaf::filter_const) in the
@@ -579,7 +583,10 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
 // Product of the transparencies of every filtered hit with EPS < d < dist (raytracer.rs:181-197).
 // Early-out once the product is exactly 0 (it stays 0: every factor is finite, checked on the
 // host), objects of transparency exactly 1.0 are skipped (x * 1.0 == x).
-template <bool SHARE = false, bool OBB = !SHARE>
+// SORDER (reflection-only kernels): walk S.strav, the likeliest occluders first (scene.cpp
+// shadow_order) -- every transparency is +-0 there, so the first filtered hit decides and the
+// order is free.
+template <bool SHARE = false, bool OBB = !SHARE, bool SORDER = OBB>
 __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
   [[maybe_unused]] constexpr int cb = 18;
   CNT(cb + 0);
@@ -590,8 +597,10 @@ __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
   const bool fin = wave_finite(p, dir);
   const double tmax = cull_tmax(dist);
   int resume = 0;
-  for (int i = 0; i < S.n_trav;) {
-    cptr<RtTrav> T = &S.trav[i];
+  const cptr<RtTrav> TR = (RT_SHADOW_ORDER && SORDER) ? S.strav : S.trav;
+  const int n_tr = (RT_SHADOW_ORDER && SORDER) ? S.n_strav : S.n_trav;
+  for (int i = 0; i < n_tr;) {
+    cptr<RtTrav> T = &TR[i];
     const bool act = i >= resume;
     if (T->obj < 0) {                                    // group node
       CNT(30);
@@ -1206,6 +1215,8 @@ __device__ __forceinline__ DS make_ds(const RtDevScene& s) {
   d.objects = as_const(s.objects);
   d.trav = as_const(s.trav);
   d.n_trav = s.n_trav;
+  d.strav = as_const(s.strav);
+  d.n_strav = s.n_strav;
   d.nodes = as_const(s.nodes);
   d.leaves = as_const(s.leaves);
   d.prog = as_const(s.prog);
@@ -1904,7 +1915,8 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   int rc = rt::flatten(*s, &f);
   if (rc) return rc;
   std::vector<uint8_t> blob;
-  size_t o_obj = put(blob, f.objects), o_trav = put(blob, f.trav), o_nodes = put(blob, f.nodes), o_leaves = put(blob, f.leaves);
+  size_t o_obj = put(blob, f.objects), o_trav = put(blob, f.trav), o_strav = put(blob, f.strav), o_nodes = put(blob, f.nodes),
+         o_leaves = put(blob, f.leaves);
   size_t o_prog = put(blob, f.prog), o_lights = put(blob, f.lights), o_tex = put(blob, f.textures);
   size_t o_texels = put(blob, f.texels);
   RT_HIP(hipSetDevice(c->device));
@@ -1918,6 +1930,8 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   d.objects = (const RtObject*)(b + o_obj);
   d.trav = (const RtTrav*)(b + o_trav);
   d.n_trav = (int32_t)f.trav.size();
+  d.strav = (const RtTrav*)(b + o_strav);
+  d.n_strav = (int32_t)f.strav.size();
   d.nodes = (const RtNode*)(b + o_nodes);
   d.leaves = (const RtLeaf*)(b + o_leaves);
   d.prog = (const RtProg*)(b + o_prog);

@@ -162,13 +162,14 @@ struct RtCamera {
 struct RtDevScene {
   const RtObject* objects;
   const RtTrav* trav;
+  const RtTrav* strav;              // shadow rays of scenes without a transparent object (any order is exact)
   const RtNode* nodes;
   const RtLeaf* leaves;
   const RtProg* prog;
   const RtLight* lights;
   const RtTexture* textures;
   const uint8_t* texels;
-  int32_t n_objects, n_lights, n_leaves, n_nodes, n_trav, pad0;
+  int32_t n_objects, n_lights, n_leaves, n_nodes, n_trav, n_strav;
   int32_t width, height;
   int32_t any_transparent;          // some object has transparency != 0 (refraction possible)
   int32_t shadow_early_out;         // every transparency is finite: product==0 stays 0

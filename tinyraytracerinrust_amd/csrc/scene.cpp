@@ -579,23 +579,25 @@ static double box_area(const double* lo, const double* hi) {
 
 struct HierBuilder {
   FlatScene& f;
+  std::vector<RtTrav>& out;
+  const std::vector<int>& perm;        // position -> object index
   void hull(int a, int b, double* lo, double* hi) const {
     for (int k = 0; k < 3; ++k) { lo[k] = INFINITY; hi[k] = -INFINITY; }
     for (int o = a; o < b; ++o)
       for (int k = 0; k < 3; ++k) {
-        lo[k] = fmin(lo[k], f.objects[o].blo[k]);
-        hi[k] = fmax(hi[k], f.objects[o].bhi[k]);
+        lo[k] = fmin(lo[k], f.objects[perm[o]].blo[k]);
+        hi[k] = fmax(hi[k], f.objects[perm[o]].bhi[k]);
       }
   }
   void object(int o) {
     RtTrav t;
     memset(&t, 0, sizeof t);
-    t.obj = o;
-    t.skip = (int32_t)f.trav.size() + 1;
-    f.trav.push_back(t);
+    t.obj = perm[o];
+    t.skip = (int32_t)out.size() + 1;
+    out.push_back(t);
   }
-  // Objects [a, b), all with a finite box.  A group node is emitted when it is clearly smaller
-  // than the enclosing group (surface area); the run is split where the SAH cost is lowest.
+  // Positions [a, b), all objects with a finite box.  A group node is emitted when it is clearly
+  // smaller than the enclosing group (surface area); the run is split where the SAH cost is lowest.
   void run(int a, int b, double parent_area) {
     if (b - a == 1) { object(a); return; }
     RtTrav g;
@@ -603,8 +605,8 @@ struct HierBuilder {
     hull(a, b, g.blo, g.bhi);
     const double area = box_area(g.blo, g.bhi);
     const bool group = area <= 0.8 * parent_area;
-    const size_t gi = f.trav.size();
-    if (group) { g.obj = -1; f.trav.push_back(g); parent_area = area; }
+    const size_t gi = out.size();
+    if (group) { g.obj = -1; out.push_back(g); parent_area = area; }
     if (b - a == 2) {
       object(a);
       object(a + 1);
@@ -621,22 +623,55 @@ struct HierBuilder {
       run(a, best_k, parent_area);
       run(best_k, b, parent_area);
     }
-    if (group) f.trav[gi].skip = (int32_t)f.trav.size();
+    if (group) out[gi].skip = (int32_t)out.size();
   }
 };
 
-static void build_hierarchy(FlatScene* fs) {
-  HierBuilder h{*fs};
-  fs->trav.clear();
-  const int n = (int)fs->objects.size();
+// The hierarchy over objects in the order `perm` (contiguous runs of finite-box objects).
+static void build_hierarchy(FlatScene* fs, const std::vector<int>& perm, std::vector<RtTrav>* out) {
+  HierBuilder h{*fs, *out, perm};
+  out->clear();
+  const int n = (int)perm.size();
   const bool flat = getenv("RT_FLAT_OBJECTS") != nullptr;   // diagnostic: no group nodes
   for (int i = 0; i < n;) {
-    if (flat || fs->objects[i].cull != RT_CULL_BOX) { h.object(i); ++i; continue; }
+    if (flat || fs->objects[perm[i]].cull != RT_CULL_BOX) { h.object(i); ++i; continue; }
     int j = i;
-    while (j < n && fs->objects[j].cull == RT_CULL_BOX) ++j;
+    while (j < n && fs->objects[perm[j]].cull == RT_CULL_BOX) ++j;
     h.run(i, j, INFINITY);
     i = j;
   }
+}
+
+// Shadow rays of a scene without a transparent object only ask whether ANY object has a filtered
+// hit in range (every transparency is +-0: the product is 0 at the first one), so their walk may
+// visit the objects in any order and stop at the first occluder.  The likeliest occluders go
+// first: objects by descending world volume of their region (the oriented box's where the object
+// has one), unbounded objects (planes) last.  With a transparent object the draw order stays
+// (the shadow product's order is the reference's).
+static std::vector<int> shadow_order(const FlatScene& f) {
+  const int n = (int)f.objects.size();
+  std::vector<int> perm(n);
+  for (int i = 0; i < n; ++i) perm[i] = i;
+  if (f.any_transparent || getenv("RT_DRAW_ORDER_SHADOWS")) return perm;
+  std::vector<double> vol(n);
+  for (int i = 0; i < n; ++i) {
+    const RtObject& o = f.objects[i];
+    if (o.cull != RT_CULL_BOX) { vol[i] = -1.0; continue; }          // unbounded: last
+    double v = 1.0;
+    for (int k = 0; k < 3; ++k) v *= o.bhi[k] - o.blo[k];
+    if (o.obb_leaf >= 0) {
+      const RtLeaf& R = f.leaves[o.obb_leaf];
+      const double* M = R.inv;
+      const double det = M[0] * (M[5] * M[10] - M[6] * M[9]) - M[1] * (M[4] * M[10] - M[6] * M[8]) +
+                         M[2] * (M[4] * M[9] - M[5] * M[8]);
+      double lv = 1.0;
+      for (int k = 0; k < 3; ++k) lv *= o.ohi[k] - o.olo[k];
+      if (std::isfinite(det) && det != 0.0) v = std::min(v, fabs(lv / det));
+    }
+    vol[i] = v;
+  }
+  std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return vol[a] > vol[b]; });
+  return perm;
 }
 
 int flatten(const rt_scene& s, FlatScene* out) {
@@ -725,7 +760,12 @@ int flatten(const rt_scene& s, FlatScene* out) {
     f.objects.push_back(ob);
   }
   for (RtObject& ob : f.objects) share_sphere_terms(f, &ob);
-  build_hierarchy(&f);
+  {
+    std::vector<int> draw((size_t)f.objects.size());
+    for (size_t i = 0; i < draw.size(); ++i) draw[i] = (int)i;
+    build_hierarchy(&f, draw, &f.trav);
+    build_hierarchy(&f, shadow_order(f), &f.strav);
+  }
   for (const LightRec& l : s.lights) {
     RtLight L;
     for (int i = 0; i < 3; ++i) { L.p[i] = l.p[i]; L.col[i] = l.color[i]; }
@@ -745,6 +785,8 @@ int flatten(const rt_scene& s, FlatScene* out) {
     for (size_t i = 0; i < f.trav.size(); ++i)
       fprintf(stderr, "trav %zu obj=%d skip=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f]\n", i, f.trav[i].obj, f.trav[i].skip,
               f.trav[i].blo[0], f.trav[i].blo[1], f.trav[i].blo[2], f.trav[i].bhi[0], f.trav[i].bhi[1], f.trav[i].bhi[2]);
+    for (size_t i = 0; i < f.strav.size(); ++i)
+      fprintf(stderr, "strav %zu obj=%d skip=%d\n", i, f.strav[i].obj, f.strav[i].skip);
     for (size_t o = 0; o < f.objects.size(); ++o) {
       const RtObject& ob = f.objects[o];
       fprintf(stderr, "object %zu cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] leaves %d leaf_cull=%d obb_leaf=%d "

@@ -41,6 +41,7 @@ struct TextureRec { uint32_t w, h; std::vector<uint8_t> rgba; };
 struct FlatScene {
   std::vector<RtObject> objects;
   std::vector<RtTrav> trav;
+  std::vector<RtTrav> strav;       // shadow-ray hierarchy: likeliest occluders first (scene.cpp build_hierarchy)
   std::vector<RtNode> nodes;
   std::vector<RtLeaf> leaves;
   std::vector<RtProg> prog;
