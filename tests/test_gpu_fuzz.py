@@ -102,3 +102,37 @@ def test_rod_scene_ordered_launches(T, seed):
     _, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H)
     for k, f in enumerate(frames):
         assert_close(f, None, ru, None, f"rod scene {seed}, launch {k}")
+
+
+_TIE_SCENES = [
+    # the same sphere drawn twice in two colours, the larger object listed second: every hit is a tie
+    "draw(plane(<0, 1, 0>, 20, white * 0.5, 0.3))\n"
+    "draw(sphere(<0, 0, 0>, 12, red, 0.4))\ndraw(sphere(<0, 0, 0>, 12, blue, 0.4))\n"
+    "draw(sphere(<-14, 4, -3>, 30, rgb(0.2, 0.8, 0.2)))\nset camera(<0, 10, -90>)\n",
+    # a small cube whose front face lies in a big cube's front face; the big cube listed first
+    "draw(plane(<0, 1, 0>, 25, red * 0.5, 0.5))\n"
+    "draw(cube(<0, 0, 0>, 40, rgb(0.7, 0.7, 0.2), 0.2))\ndraw(cube(<0, 0, -10>, 20, blue, 0.2))\n"
+    "set camera(<5, 12, -95>)\n",
+    # rotated duplicates (one object through a CSG union with itself) and a shared tilted plane
+    "rotate(0.3, 0.5, 0.1) do\n  a = sphere(<3, 0, 0>, 10)\n  draw(csg(a, a, 'union', red, 0.5))\n"
+    "  draw(sphere(<3, 0, 0>, 10, white, 0.5))\nend\n"
+    "draw(plane(<0.2, 1, 0.1>, 22, blue * 0.6, 0.4))\ndraw(plane(<0.2, 1, 0.1>, 22, red * 0.6, 0.4))\n",
+]
+
+
+@pytest.mark.parametrize("k", range(len(_TIE_SCENES)))
+def test_nearest_hit_ties_follow_draw_order(T, k):
+    """Objects with coincident surfaces: the reference keeps the first object in draw order that
+    reaches the nearest distance (raytracer.rs:141-150); the reflection-only kernels visit objects
+    largest-first and resolve equal distances by draw order -- every pixel as the oracle's."""
+    from oracle import oracle as O
+    text = _TIE_SCENES[k]
+    W, H, d = 160, 120, 6
+    rt = T.RayTracer(W, H)
+    rt.max_depth = d
+    rt.load_scene(text, 0.0)
+    gu = rt.renderer.render_rows_host(0, H)
+    gf = rt.renderer.render_rows_host(0, H, f64=True)
+    rf, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H, f64=True)
+    assert_close(gu, gf, ru, rf, f"tie scene {k}")
+    assert np.array_equal(gu, ru)

@@ -162,6 +162,9 @@ constexpr double EPS = RT_EPSILON;
 #ifndef RT_PLANE_AXIS
 #define RT_PLANE_AXIS 1             // axis-aligned planes: one product per dot in the traversals
 #endif
+#ifndef RT_NEAREST_ORDER
+#define RT_NEAREST_ORDER 1          // reflection-only kernels: nearest-hit walk in the shadow walk's order (tie-exact)
+#endif
 #ifndef RT_SHADOW_ORDER
 #define RT_SHADOW_ORDER 1           // reflection-only kernels: shadow rays walk the likeliest occluders first
 #endif
@@ -533,8 +536,15 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
   const CullRay cr = cull_ray(ro, rd);
   const bool fin = wave_finite(ro, rd);
   int resume = 0;
-  for (int i = 0; i < S.n_trav;) {
-    cptr<RtTrav> T = &S.trav[i];
+  // NORDER (reflection-only kernels): the objects in S.strav's order, largest regions first, so an
+  // early hit on a big object culls what lies behind it.  Exact: a candidate equal to the best
+  // distance so far wins when its object comes earlier in DRAW order (o < bobj), which is the
+  // reference's first-visited-wins rule (raytracer.rs:141-150) for any visiting order.
+  constexpr bool NORDER = RT_NEAREST_ORDER && OBB;
+  const cptr<RtTrav> TR = NORDER ? S.strav : S.trav;
+  const int n_tr = NORDER ? S.n_strav : S.n_trav;
+  for (int i = 0; i < n_tr;) {
+    cptr<RtTrav> T = &TR[i];
     const bool act = i >= resume;
     if (T->obj < 0) {                                    // group node
       CNT(28 + cat);
@@ -568,10 +578,12 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
       int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1, SHARE ? &shr : nullptr);
       const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && SHARE && L->filter_const && !isnan(cr.inv.x));
       if (filtered && ((n >= 1 && t0 > EPS && t0 < best) || (n >= 2 && t1 > EPS))) CNT(cb + 8);
-      if (n >= 1 && t0 > EPS && t0 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) {
+      if (n >= 1 && t0 > EPS && (t0 < best || (NORDER && t0 == best && o < bobj)) &&
+          (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) {
         best = t0; bobj = o;
       }
-      if (n >= 2 && t1 > EPS && t1 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t1))))) {
+      if (n >= 2 && t1 > EPS && (t1 < best || (NORDER && t1 == best && o < bobj)) &&
+          (!filtered || leaf_filter(S, L, add(ro, scale(rd, t1))))) {
         best = t1; bobj = o;
       }
     }
