@@ -102,9 +102,10 @@ def parse():
                     help="priority of RCCL's stream (the all-gathers) relative to the render streams")
     ap.add_argument("--pool-streams", action="store_true",
                     help="diagnostic: frames in flight on torch pool streams instead of own-queue streams")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=4,
                     help="anim120: frames dealt round-robin over this many HIP streams so independent "
-                         "frames' kernels overlap (one 1080p frame does not fill the GPU to its end)")
+                         "frames' kernels overlap (one 1080p frame does not fill the GPU to its end); "
+                         "1 / 2 / 3 / 4 streams: 8226 / 8786 / 8901 / 8913 Mrays/s (profiles/r02cu_anim120_streams.txt)")
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="before the warmup steps, render untimed frames for this long so the GPU reaches its "
                          "sustained clocks (reported as `settle` in the line; 0 disables).  Measured: 20 steps after "
