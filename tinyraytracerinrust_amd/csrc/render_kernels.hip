@@ -162,6 +162,9 @@ constexpr double EPS = RT_EPSILON;
 #ifndef RT_PLANE_AXIS
 #define RT_PLANE_AXIS 1             // axis-aligned planes: one product per dot in the traversals
 #endif
+#ifndef RT_OBB_REFR
+#define RT_OBB_REFR 0               // 1: oriented object boxes (and the strav walks) in the refraction kernels too
+#endif
 #ifndef RT_NEAREST_ORDER
 #define RT_NEAREST_ORDER 1          // reflection-only kernels: nearest-hit walk in the shadow walk's order (tie-exact)
 #endif
@@ -886,7 +889,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
   // reflection-only megakernel at 5 waves spills 14 more VGPRs and runs 6 % slower on 4K globes
   // (profiles/r02am_ab.txt).
   constexpr bool SHARE = (REFR || RT_SHARE_MEGA) && RT_SPHERE_SHARE;
-  constexpr bool OBB = !REFR;                          // oriented object boxes: reflection-only kernels
+  constexpr bool OBB = !REFR || RT_OBB_REFR;           // oriented object boxes: reflection-only kernels
   int fSlot[RECORD ? RT_MAX_DEPTH_CAP : 1];
   [[maybe_unused]] int ray_type = 0, slot = 0;                  // RayType::NormalRay
   int sp = 0, depth = 0;
