@@ -287,6 +287,10 @@ def main():
     rt = T.RayTracer(W, H, device=local)
     rt.load_scene(text, t, asset_dir=SCENES)
     rend = rt.renderer                                    # uploads the scene blob + texture
+    # bench times the launches with its own events on the launch stream: the library's per-launch
+    # event pair (rt_ctx_last_kernel_ms) is off, as a host that does not read it would run
+    # (RT_OPT_TIMING: each timed event costs the stream ~5 us, profiles/r02dc_launch_events.txt)
+    rend.set_timing(False)
 
     layout = a.layout if multi else "contiguous"
     band = a.band if layout == "cyclic" else -(-H // world)
@@ -618,6 +622,7 @@ def anim_main(a, json_out, rank, world, local, dev, multi):
         sc = T.Scene.compile(text, f / F, W, H, asset_dir=SCENES)
         r = T.Renderer(local)
         r.upload(sc)
+        r.set_timing(False)                               # bench's own events time the frames
         rends.append(r)
     torch.cuda.synchronize(dev)
     prep_ms = (time.perf_counter() - t0) * 1e3 / max(1, len(mine))

@@ -224,7 +224,7 @@ int rt_antialias(rt_ctx* ctx, const uint8_t* src_rgba8, size_t src_stride, doubl
                  int32_t max_depth, uint8_t* dst_rgba8, size_t dst_stride, double* dst_f64, size_t f64_stride,
                  uint64_t* rays_traced, void* stream);
 /* Milliseconds of the last render launch on this context (HIP events recorded on the launch's
- * stream around the kernel). */
+ * stream around the kernel; RT_OPT_TIMING 0 turns them off and this call then fails). */
 int rt_ctx_last_kernel_ms(rt_ctx* ctx, float* ms);
 int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launch */
 /* Tuning options of a context.  No option changes a single pixel; they only choose how the
@@ -236,8 +236,12 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  *     streams (their launches overlap, so no launch's tail leaves the GPU idle);
  *   RT_KERNEL_DEFERRED: always the deferred-shadow kernel.
  * Changing the kernel drops the context's tile orders (the next launch of each geometry
- * calibrates again).  Scenes with a transparent object always take the refraction megakernel. */
-typedef enum rt_option { RT_OPT_KERNEL = 0 } rt_option;
+ * calibrates again).  Scenes with a transparent object always take the refraction megakernel.
+ * RT_OPT_TIMING: 1 (default) records a HIP event pair around every render launch for
+ * rt_ctx_last_kernel_ms; 0 records none.  Each timed event costs the stream ~5 us on MI355X
+ * (a 1080p single-sphere frame: 0.045 -> 0.036 ms per launch without them), so a host that
+ * times its own stream, or does not time at all, turns them off. */
+typedef enum rt_option { RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1 } rt_option;
 typedef enum rt_kernel_choice { RT_KERNEL_AUTO = 0, RT_KERNEL_MEGA = 1, RT_KERNEL_DEFERRED = 2 } rt_kernel_choice;
 int rt_ctx_set_option(rt_ctx* ctx, int32_t option, int32_t value);
 void rt_ctx_free(rt_ctx* ctx);

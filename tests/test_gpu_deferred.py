@@ -69,3 +69,27 @@ def test_kernel_option_same_pixels():
     from tinyraytracerinrust_amd import _lib
     with pytest.raises(T.RtError):
         _lib.check(T.lib().rt_ctx_set_option(r.h, 0, 7))
+
+
+def test_timing_option():
+    """rt_ctx_set_option(RT_OPT_TIMING): with the launch events off the frames are the same and
+    rt_ctx_last_kernel_ms fails; turned back on, the next launch is timed again."""
+    import numpy as np
+    import tinyraytracerinrust_amd as T
+    from tinyraytracerinrust_amd import _lib
+    from tests.conftest import SCENES, scene_text
+    W, H = 320, 240
+    rt = T.RayTracer(W, H)
+    rt.load_scene(scene_text("globes"), 0.0, asset_dir=SCENES)
+    r = rt.renderer
+    ref = r.render_rows_host(0, H)
+    assert r.last_kernel_ms() > 0.0
+    r.set_timing(False)
+    assert np.array_equal(r.render_rows_host(0, H), ref)
+    with pytest.raises(T.RtError):
+        r.last_kernel_ms()
+    r.set_timing(True)
+    assert np.array_equal(r.render_rows_host(0, H), ref)
+    assert r.last_kernel_ms() > 0.0
+    with pytest.raises(T.RtError):
+        _lib.check(T.lib().rt_ctx_set_option(r.h, _lib.RT_OPT_TIMING, 2))

@@ -20,6 +20,7 @@ STATUS_NAMES = {
 }
 RT_CSG_UNION, RT_CSG_INTERSECTION, RT_CSG_DIFFERENCE = 0, 1, 2
 RT_OPT_KERNEL = 0
+RT_OPT_TIMING = 1
 RT_KERNEL_AUTO, RT_KERNEL_MEGA, RT_KERNEL_DEFERRED = 0, 1, 2
 
 

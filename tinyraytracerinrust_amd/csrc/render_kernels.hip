@@ -1717,6 +1717,7 @@ struct rt_ctx {
   RtDevScene dev;
   int32_t max_depth = 10;
   int32_t kernel_opt = RT_KERNEL_AUTO;  // rt_ctx_set_option(RT_OPT_KERNEL)
+  bool timing = true;                   // rt_ctx_set_option(RT_OPT_TIMING): launch events recorded
   bool uploaded = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -2041,7 +2042,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   else if (order) deferred = slot->deferred;
   else if (calibrate) deferred = false;                       // calibrate on the megakernel
   else deferred = n_tiles < RT_ORDER_MIN_TILES || (!tile_order_enabled() && n_tiles < deferred_max_tiles());
-  RT_HIP(hipEventRecord(c->ev0, st));
+  if (c->timing) RT_HIP(hipEventRecord(c->ev0, st));
 #define RT_LAUNCH_ROWS(R, F)                                                                                  \
   if (calibrate && fc) hipLaunchKernelGGL((render_rows_kernel<R, F, true, true>), grid, block, 0, st, c->dev, a0, a1, \
                                           a2, a3, max_depth, target, tstride, order, cost, rgbi);                       \
@@ -2070,8 +2071,8 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
 #undef RT_LAUNCH_ROWS
 #undef RT_LAUNCH_DEFERRED
   RT_HIP(hipGetLastError());
-  RT_HIP(hipEventRecord(c->ev1, st));
-  c->timed = true;
+  if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
+  c->timed = c->timing;
   if (calibrate) {                    // synchronous, once per geometry and scene upload
     std::vector<uint32_t> h_cost(n_tiles);
     std::vector<int32_t> h_order(n_tiles);
@@ -2279,7 +2280,7 @@ int rt_antialias(rt_ctx* c, const uint8_t* src_rgba8, size_t src_stride, double 
   uint32_t* edges = (uint32_t*)(sb + o_edges);
   uint32_t* cnt = (uint32_t*)(sb + o_cnt);
   RT_HIP(hipMemsetAsync(cnt, 0, 64, st));
-  RT_HIP(hipEventRecord(c->ev0, st));
+  if (c->timing) RT_HIP(hipEventRecord(c->ev0, st));
   const int tiles = ((W + 15) / 16) * ((H + 15) / 16);
   hipLaunchKernelGGL(aa_classify_kernel, dim3(tiles), dim3(256), 0, st, src, sstride, W, H, threshold, (int)level,
                      u8, u8s, f64, f64s, edges, cnt);
@@ -2334,8 +2335,8 @@ int rt_antialias(rt_ctx* c, const uint8_t* src_rgba8, size_t src_stride, double 
     (void)hipFreeAsync(work, st);
     if (err) return err;
   }
-  RT_HIP(hipEventRecord(c->ev1, st));
-  c->timed = true;
+  if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
+  c->timed = c->timing;
   if (dst_rgba8 && !d_u8) RT_HIP(hipMemcpy2DAsync(dst_rgba8, dst_stride, u8, row4, row4, H, hipMemcpyDeviceToHost, st));
   if (dst_f64 && !d_f64) RT_HIP(hipMemcpy2DAsync(dst_f64, f64_stride, f64, row32, row32, H, hipMemcpyDeviceToHost, st));
   RT_HIP(hipStreamSynchronize(st));
@@ -2378,11 +2379,11 @@ int rt_render_ortho(rt_ctx* c, int32_t axis1, int32_t axis2, double dir1, double
     if (!df) { tf = (double*)sb; sf = row32; }
   }
   const int tiles = ((W + 15) / 16) * (int)((n + 15) / 16);
-  RT_HIP(hipEventRecord(c->ev0, st));
+  if (c->timing) RT_HIP(hipEventRecord(c->ev0, st));
   hipLaunchKernelGGL(ortho_kernel, dim3(tiles), dim3(256), 0, st, c->dev, V, (int)y0, (int)n, t8, s8, tf, sf);
   RT_HIP(hipGetLastError());
-  RT_HIP(hipEventRecord(c->ev1, st));
-  c->timed = true;
+  if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
+  c->timed = c->timing;
   if (!d8) RT_HIP(hipMemcpy2DAsync(rgba8, row_stride_bytes, t8, row4, row4, n, hipMemcpyDeviceToHost, st));
   if (!df) RT_HIP(hipMemcpy2DAsync(rgba_f64, f64_stride, tf, row32, row32, n, hipMemcpyDeviceToHost, st));
   if (!d8 || !df) RT_HIP(hipStreamSynchronize(st));
@@ -2449,12 +2450,12 @@ int rt_render_points_f64(rt_ctx* c, const double* xy, size_t n, int32_t max_dept
     if (!dev_out) target = sx + 2 * n;
   }
   dim3 grid((unsigned)((n + 255) / 256)), block(256);
-  RT_HIP(hipEventRecord(c->ev0, st));
+  if (c->timing) RT_HIP(hipEventRecord(c->ev0, st));
   if (c->dev.any_transparent) hipLaunchKernelGGL((render_points_kernel<true>), grid, block, 0, st, c->dev, in, n, max_depth, target);
   else hipLaunchKernelGGL((render_points_kernel<false>), grid, block, 0, st, c->dev, in, n, max_depth, target);
   RT_HIP(hipGetLastError());
-  RT_HIP(hipEventRecord(c->ev1, st));
-  c->timed = true;
+  if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
+  c->timed = c->timing;
   if (!dev_out) {
     RT_HIP(hipMemcpyAsync(out, target, n * 4 * sizeof(double), hipMemcpyDeviceToHost, st));
     RT_HIP(hipStreamSynchronize(st));
@@ -2464,7 +2465,7 @@ int rt_render_points_f64(rt_ctx* c, const double* xy, size_t n, int32_t max_dept
 
 int rt_ctx_last_kernel_ms(rt_ctx* c, float* ms) {
   if (!c || !ms) return fail(RT_ERR_INVALID, "null argument");
-  if (!c->timed) return fail(RT_ERR_INVALID, "no launch recorded");
+  if (!c->timed) return fail(RT_ERR_INVALID, c->timing ? "no launch recorded" : "RT_OPT_TIMING is off");
   RT_HIP(hipEventSynchronize(c->ev1));
   RT_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
   return RT_OK;
@@ -2472,6 +2473,12 @@ int rt_ctx_last_kernel_ms(rt_ctx* c, float* ms) {
 
 int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
   if (!c) return fail(RT_ERR_INVALID, "null context");
+  if (option == RT_OPT_TIMING) {
+    if (value != 0 && value != 1) return fail(RT_ERR_INVALID, "RT_OPT_TIMING value %d", value);
+    c->timing = value != 0;
+    c->timed = false;                  // no launch recorded under the new setting yet
+    return RT_OK;
+  }
   if (option != RT_OPT_KERNEL) return fail(RT_ERR_INVALID, "unknown option %d", option);
   if (value != RT_KERNEL_AUTO && value != RT_KERNEL_MEGA && value != RT_KERNEL_DEFERRED)
     return fail(RT_ERR_INVALID, "RT_OPT_KERNEL value %d", value);

@@ -280,6 +280,11 @@ class Renderer:
         v = {"auto": _lib.RT_KERNEL_AUTO, "mega": _lib.RT_KERNEL_MEGA, "deferred": _lib.RT_KERNEL_DEFERRED}[kernel]
         check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_KERNEL, v))
 
+    def set_timing(self, on: bool) -> None:
+        """rt_ctx_set_option(RT_OPT_TIMING): record (default) or skip the HIP event pair around every
+        render launch that last_kernel_ms() reads (each timed event costs the stream ~5 us)."""
+        check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_TIMING, 1 if on else 0))
+
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()
         check(lib().rt_ctx_last_kernel_ms(self.h, ctypes.byref(ms)))
