@@ -391,9 +391,12 @@ def main():
     # timed region, and the kernel time per launch is its span / K -- a timed event costs the
     # stream ~5 us (profiles/r02dc_launch_events.txt), so events around every launch would slow the
     # launches they measure.  Otherwise (several streams, or the collective path) a pair per step.
+    # With frames in flight (K > 1) the roofline is taken over wall time and per-step events would
+    # only add their cost to every render stream: none are recorded then.
     region = K == 1 and not multi
-    evs = [] if region else [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                             for _ in range(a.steps)]
+    per_step = K == 1 and multi
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)] \
+        if per_step else []
     reg = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     if multi:
         dist.barrier()
@@ -414,7 +417,8 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    kernel_ms = [s.elapsed_time(e) for s, e in evs] if evs else [reg[0].elapsed_time(reg[1]) / a.steps]
+    kernel_ms = ([s.elapsed_time(e) for s, e in evs] if evs else
+                 [reg[0].elapsed_time(reg[1]) / a.steps] if region else [elapsed * 1e3 / a.steps])
     mean_kernel_ms = sum(kernel_ms) / len(kernel_ms)
     rows_per_rank = None
     # outside the timed region: every frame buffer holds one of the last frames (assembled, at
@@ -488,8 +492,8 @@ def main():
             "kernel_ms_mean": round(mean_kernel_ms, 4),
             "achieved_basis": ("kernel time: one event pair over the K back-to-back launches on the launch stream / K"
                                if region else "kernel event time per launch" if K == 1
-                               else f"step wall time ({K} frames in flight)"),
-            "kernel_ms_min": None if region else round(min(kernel_ms), 4),
+                               else f"step wall time ({K} frames in flight; no per-step events)"),
+            "kernel_ms_min": round(min(kernel_ms), 4) if per_step else None,
             "algorithmic_flops_per_launch": flops_launch,
             "frac_of_no_fma_ceiling": round(achieved / FP64_NO_FMA_TFLOPS, 4) if achieved else None,
             "no_fma_ceiling": FP64_NO_FMA_TFLOPS,
