@@ -263,8 +263,8 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: one rank per GPU")
     rehearse = a.rehearse_one_gpu
     if rehearse:
-        if a.config in ANIM or not launched:
-            raise SystemExit("--rehearse-one-gpu: a frame config under a launcher (--gpus N > 1 starts one)")
+        if not launched:
+            raise SystemExit("--rehearse-one-gpu: under a launcher (--gpus N > 1 starts one)")
         local = 0                        # every rank on the one GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -280,7 +280,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev, pg_options=opts)
 
     if a.config in ANIM:
-        return anim_main(a, json_out, rank, world, local, dev, multi)
+        return anim_main(a, json_out, rank, world, local, dev, multi, rehearse)
     scene, W, H, t, depth = CONFIGS[a.config]
     text = open(os.path.join(SCENES, scene + ".scene")).read() if scene else SPHERE_SCENE
     scene = scene or "sphere"
@@ -620,12 +620,17 @@ def launcher_check(a, json_out):
         sys.exit(1)
 
 
-def anim_main(a, json_out, rank, world, local, dev, multi):
+def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
     """BASELINE config 5: frames f = 0..F-1 of spinning_globes.scene at time f / F, rank r
-    renders f = r (mod N) -- replicas, no collective.  Each owned frame's scene is compiled and
-    uploaded once before the timed region (host compile + H2D upload are timed and reported
-    separately, like the headline's); one step renders every frame of the animation into its own
-    HBM framebuffer."""
+    renders f = r (mod N) -- replicas, no collective (the reference's animate mode renders its
+    frames as independent pool jobs, src/raydebugger/gui.rs:78-89, each with its own scene build,
+    debug_window.rs:53-62).  Each owned frame's scene is compiled and uploaded once before the
+    timed region (host compile + H2D upload are timed and reported separately, like the
+    headline's); one step renders every frame of the animation into its own HBM framebuffer.
+    After the timed region every rank compares EVERY owned frame buffer with a single-launch render
+    of that frame on the default stream (catches stream-ordering and buffer-reuse mistakes of the
+    overlapping streams).  ``--rehearse-one-gpu``: every rank on device 0, gloo process group, no
+    value."""
     import torch
     import torch.distributed as dist
     import tinyraytracerinrust_amd as T
@@ -680,11 +685,26 @@ def anim_main(a, json_out, rank, world, local, dev, multi):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if multi:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     per_frame = [sum(evs[i][j][0].elapsed_time(evs[i][j][1]) for i in range(a.steps)) / a.steps
                  for j in range(len(mine))]
+    # outside the timed region: every owned frame buffer == a single-launch render of its frame
+    bad = []
+    for j, r in enumerate(rends):
+        whole = r.render_rows(0, H, max_depth=depth)
+        torch.cuda.synchronize(dev)
+        if not torch.equal(outs[j], whole):
+            bad.append(mine[j])
+    if bad:
+        raise SystemExit(f"rank {rank}: frame buffer(s) of frames {bad} differ from the single-launch render")
+    frame_check = f"all {len(mine)} frame buffers == single-launch render" + (", on every rank" if multi else "")
+    frames_per_rank = None
+    if multi:
+        counts = [None] * world
+        dist.all_gather_object(counts, mine)
+        frames_per_rank = counts
     if rank != 0:
         if multi:
             dist.destroy_process_group()
@@ -739,7 +759,15 @@ def anim_main(a, json_out, rank, world, local, dev, multi):
         "host_compile_upload_ms_per_frame": round(prep_ms, 3),
         "settle": settle,
         "cpu_baseline": None,
+        "frame_check": frame_check,
     }
+    if multi:
+        line["distributed"] = {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(),
+                               "frames_per_rank": [len(c) for c in frames_per_rank],
+                               "frames_of_rank": frames_per_rank, "frame_check": frame_check}
+    if rehearse:
+        line.update({"metric": "one-GPU rehearsal of the N-rank animation (not a measurement)", "value": None,
+                     "vs_baseline": None, "roofline": None, "rays": None})
     if world == 1 and not multi and not a.no_cpu_baseline:
         from oracle import oracle as O
         cores, model, aff, quota = host_cpus()

@@ -240,8 +240,13 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  * RT_OPT_TIMING: 1 (default) records a HIP event pair around every render launch for
  * rt_ctx_last_kernel_ms; 0 records none.  Each timed event costs the stream ~5 us on MI355X
  * (a 1080p single-sphere frame: 0.045 -> 0.036 ms per launch without them), so a host that
- * times its own stream, or does not time at all, turns them off. */
-typedef enum rt_option { RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1 } rt_option;
+ * times its own stream, or does not time at all, turns them off.
+ * RT_OPT_TILE_ORDER: 1 (default) dispatches the tiles of a geometry longest-first after one
+ * calibration launch (a host synchronisation per new geometry); 0 dispatches row-major.
+ * RT_OPT_FAST_CLAMP: 1 (default) lets the kernels clamp colours with min/max where the host proved
+ * it bit-identical to the reference's compare/select clamp (RtDevScene::colour_fast); 0 keeps the
+ * compare/select form everywhere (A/B checks). */
+typedef enum rt_option { RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3 } rt_option;
 typedef enum rt_kernel_choice { RT_KERNEL_AUTO = 0, RT_KERNEL_MEGA = 1, RT_KERNEL_DEFERRED = 2 } rt_kernel_choice;
 int rt_ctx_set_option(rt_ctx* ctx, int32_t option, int32_t value);
 void rt_ctx_free(rt_ctx* ctx);

@@ -1,59 +1,59 @@
 """The deferred-shadow path (render_kernels.hip trace_deferred: chain phase, wave-wide shadow
-phase through an LDS window, post-order fold) on EVERY tile -- RT_DEFERRED=1, which the library
-reads once per process, so the check runs in a child process -- against the oracle
-(src/raytracer/raytracer.rs:132-287): small frames (no ordered launch, lanes outside the frame
-trace other lanes' shadow rays) and ordered frames whose costliest tiles are split over several
-waves."""
-import os
-import subprocess
-import sys
-
+phase through an LDS window, post-order fold) on EVERY tile -- rt_ctx_set_option(RT_OPT_KERNEL,
+RT_KERNEL_DEFERRED) -- against the oracle (src/raytracer/raytracer.rs:132-287): small frames (no
+ordered launch, lanes outside the frame trace other lanes' shadow rays) and ordered frames whose
+costliest tiles are split over several waves."""
+import numpy as np
 import pytest
 
-from tests.conftest import ROOT
+from tests.conftest import SCENES, scene_text
 
 pytestmark = pytest.mark.gpu
 
-CHILD = r"""
-import sys
-sys.path.insert(0, ROOT)
-import numpy as np
-import tinyraytracerinrust_amd as T
-from oracle import oracle as O
-from tests.conftest import SCENES, scene_text
-O.register_texture_file("worldmap.png", SCENES + "/worldmap.png")
-cases = [("globes", 0.0, 64, 48, 10), ("globes", 0.25, 161, 121, 10), ("globes", 0.0, 640, 480, 10),
+CASES = [("globes", 0.0, 64, 48, 10), ("globes", 0.25, 161, 121, 10), ("globes", 0.0, 640, 480, 10),
          ("globes", 0.5, 640, 480, 3), ("three_cubes", 0.0, 160, 120, 10), ("spinning_cube", 0.3, 160, 120, 10),
          ("ground_star", 0.2, 160, 120, 10), ("spinning_gimbals", 0.4, 160, 120, 10), ("fractal", 0.0, 96, 72, 10)]
-for name, t, W, H, d in cases:
+
+
+@pytest.mark.parametrize("name,t,W,H,d", CASES)
+def test_every_tile_on_the_deferred_path(worldmap, name, t, W, H, d):
+    import tinyraytracerinrust_amd as T
+    from oracle import oracle as O
     rt = T.RayTracer(W, H)
     rt.max_depth = d
     rt.load_scene(scene_text(name), t, asset_dir=SCENES)
+    rt.renderer.set_kernel("deferred")
     frames = [rt.renderer.render_rows_host(0, H) for _ in range(2)]     # calibration (if ordered), ordered
     f64 = rt.renderer.render_rows_host(0, H, f64=True)
     rf, ru = O.OracleScene(scene_text(name), t, W, H, max_depth=d).render(0, H, f64=True)
     for u in frames:
         assert np.array_equal(u, ru), (name, t, W, H, int((u != ru).sum()))
     assert np.nanmax(np.abs(f64 - rf)) <= 1e-9, name
-    print("ok", name, t, W, H, d, flush=True)
-"""
 
 
-def test_every_tile_on_the_deferred_path():
-    env = dict(os.environ, RT_DEFERRED="1")
-    p = subprocess.run([sys.executable, "-c", f"ROOT = {ROOT!r}\n" + CHILD], env=env, cwd=ROOT,
-                       capture_output=True, text=True, timeout=240)
-    print(p.stdout)
-    assert p.returncode == 0, p.stderr[-4000:]
-    assert p.stdout.count("ok ") == 9
+def test_deferred_request_beyond_split_encoding_takes_megakernel():
+    """The deferred kernel's order entries hold a tile index in 20 bits: a launch of more than 2^20
+    tiles must fall back to the megakernel even when the deferred kernel is requested (same pixels)."""
+    import torch
+    import tinyraytracerinrust_amd as T
+    W, H = 8200, 8200                                # 1025 x 1025 = 1 050 625 tiles > 2^20
+    text = "draw(sphere(<0, 0, 0>, 30, red))"
+    frames = {}
+    for mode in ("mega", "deferred"):
+        rt = T.RayTracer(W, H)
+        rt.max_depth = 0
+        rt.load_scene(text, 0.0)
+        rt.renderer.set_kernel(mode)
+        frames[mode] = rt.renderer.render_rows(0, H)
+        torch.cuda.synchronize()
+    assert torch.equal(frames["mega"], frames["deferred"])
+    assert int((frames["mega"][..., 0] > 0).sum()) > 0
 
 
 def test_kernel_option_same_pixels():
     """rt_ctx_set_option(RT_OPT_KERNEL): auto / megakernel / deferred give identical frames on one
     context, including after switching back and forth (tile orders are rebuilt per kernel)."""
-    import numpy as np
     import tinyraytracerinrust_amd as T
-    from tests.conftest import SCENES, scene_text
     W, H = 640, 480                                  # >= 2048 tiles: ordered (and split) launches
     rt = T.RayTracer(W, H)
     rt.load_scene(scene_text("globes"), 0.25, asset_dir=SCENES)
@@ -74,10 +74,8 @@ def test_kernel_option_same_pixels():
 def test_timing_option():
     """rt_ctx_set_option(RT_OPT_TIMING): with the launch events off the frames are the same and
     rt_ctx_last_kernel_ms fails; turned back on, the next launch is timed again."""
-    import numpy as np
     import tinyraytracerinrust_amd as T
     from tinyraytracerinrust_amd import _lib
-    from tests.conftest import SCENES, scene_text
     W, H = 320, 240
     rt = T.RayTracer(W, H)
     rt.load_scene(scene_text("globes"), 0.0, asset_dir=SCENES)

@@ -65,3 +65,25 @@ def test_rehearsal_n_ranks_on_one_gpu(world, inflight, layout):
     k = inflight or 4
     assert d["frames_in_flight"] == k
     assert d["frame_check"] == f"all {k + 1} frame buffers == single-launch render, on every rank"
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_rehearsal_animation_ranks_on_one_gpu(world):
+    """BASELINE config 5 as the driver runs it (`python bench.py --gpus N --config anim120`: frames
+    dealt round-robin, f = rank (mod N), src/raydebugger/gui.rs:78-89) with every rank on the one
+    GPU of this box: each rank compiles and uploads its frames, renders them on its own-queue
+    streams, and after the timed region checks EVERY owned frame buffer against a single-launch
+    render of that frame."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
+           "--config", "anim120", "--steps", "2", "--warmup", "1", "--settle-ms", "0", "--streams", "2"]
+    p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd=ROOT, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([l for l in p.stdout.splitlines() if l.strip()][-1])
+    assert line["value"] is None and line["n_gpus"] == world
+    d = line["distributed"]
+    assert d["backend"] == "gloo" and d["world_size_seen"] == world
+    assert d["frames_per_rank"] == [len(range(r, 120, world)) for r in range(world)]
+    assert d["frames_of_rank"] == [list(range(r, 120, world)) for r in range(world)]
+    assert d["frame_check"] == f"all {len(range(0, 120, world))} frame buffers == single-launch render, on every rank"

@@ -53,6 +53,8 @@ def _parse(argv):
         ap.error("--size must be positive")
     if a.gpus < 1:
         ap.error("--gpus must be >= 1")
+    if a.band < 1:
+        ap.error("--band must be >= 1")
     a.t = a.frame / 300.0 if a.frame is not None else (a.time or 0.0)
     return a
 

@@ -21,6 +21,8 @@ STATUS_NAMES = {
 RT_CSG_UNION, RT_CSG_INTERSECTION, RT_CSG_DIFFERENCE = 0, 1, 2
 RT_OPT_KERNEL = 0
 RT_OPT_TIMING = 1
+RT_OPT_TILE_ORDER = 2
+RT_OPT_FAST_CLAMP = 3
 RT_KERNEL_AUTO, RT_KERNEL_MEGA, RT_KERNEL_DEFERRED = 0, 1, 2
 
 
@@ -123,10 +125,12 @@ def lib() -> ctypes.CDLL:
     # (same SONAMEs as /opt/rocm's).  Loaded after torch, this library binds to torch's copies;
     # loaded first, it would pull in /opt/rocm's, and torch's runtime, started later on top of an
     # HSA runtime of another release, finds no device (torch.cuda.is_available() -> False).
-    try:
-        import torch  # noqa: F401
-    except ImportError:                               # a host without torch: /opt/rocm's runtime
-        pass
+    # RT_NO_TORCH_PRELOAD=1 skips this (a host that never uses torch binds /opt/rocm's runtime).
+    if not os.environ.get("RT_NO_TORCH_PRELOAD"):
+        try:
+            import torch  # noqa: F401
+        except Exception:                             # no (working) torch: /opt/rocm's runtime
+            pass
     handle = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(handle, name)

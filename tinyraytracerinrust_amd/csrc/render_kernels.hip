@@ -154,16 +154,8 @@ struct DS {                         // device view of RtDevScene
 };
 
 constexpr double EPS = RT_EPSILON;
-#ifndef RT_LIGHT_GROUP
-#define RT_LIGHT_GROUP 1            // shadow transparencies held in registers per light group: 1 frees
-                                    // the registers that let reflection-only scenes run 7 waves/SIMD
-                                    // (profiles/r01ad_ab_light_group.txt)
-#endif
 #ifndef RT_PLANE_AXIS
 #define RT_PLANE_AXIS 1             // axis-aligned planes: one product per dot in the traversals
-#endif
-#ifndef RT_OBB_REFR
-#define RT_OBB_REFR 0               // 1: oriented object boxes (and the strav walks) in the refraction kernels too
 #endif
 #ifndef RT_NEAREST_ORDER
 #define RT_NEAREST_ORDER 1          // reflection-only kernels: nearest-hit walk in the shadow walk's order (tie-exact)
@@ -177,15 +169,8 @@ constexpr double EPS = RT_EPSILON;
                                     // in the reflection-only megakernel the test cost 4 more spilled VGPRs
                                     // (profiles/r02co_const_filter_ab.txt)
 #endif
-#ifndef RT_SHARE_MEGA
-#define RT_SHARE_MEGA 0             // 1: shared sphere terms in the reflection-only kernels too: 7-8 % slower
-                                    // (20 spilled VGPRs, profiles/r02cm_share_mega_ab.txt)
-#endif
 #ifndef RT_SPHERE_SHARE
 #define RT_SPHERE_SHARE 1           // concentric sphere leaves with one transform share their ray terms
-#endif
-#ifndef RT_REUSE_SDIR
-#define RT_REUSE_SDIR 1             // one light direction per (hit, light) for the shadow ray and Lambert
 #endif
 constexpr double PI_D = 3.14159265358979323846;   // std::f64::consts::PI
 
@@ -888,8 +873,8 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
   // the registers (104 -> 116 VGPRs, no spill; spinning_globes 1080p 4.8 % faster), while the
   // reflection-only megakernel at 5 waves spills 14 more VGPRs and runs 6 % slower on 4K globes
   // (profiles/r02am_ab.txt).
-  constexpr bool SHARE = (REFR || RT_SHARE_MEGA) && RT_SPHERE_SHARE;
-  constexpr bool OBB = !REFR || RT_OBB_REFR;           // oriented object boxes: reflection-only kernels
+  constexpr bool SHARE = REFR && RT_SPHERE_SHARE;
+  constexpr bool OBB = !REFR;                          // oriented object boxes: reflection-only kernels
   int fSlot[RECORD ? RT_MAX_DEPTH_CAP : 1];
   [[maybe_unused]] int ray_type = 0, slot = 0;                  // RayType::NormalRay
   int sp = 0, depth = 0;
@@ -917,7 +902,6 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
       // normal / UV / material and the per-light Lambert terms are formed afterwards: far fewer
       // registers live across the traversals.  Light accumulation order is unchanged.
       bool have_shading = false;
-#if RT_LIGHT_GROUP == 1 && RT_REUSE_SDIR
       // One light at a time: the unit vector towards the light is the shadow ray's direction
       // (:176-178) AND the Lambert term's `sdir` (:203-205), the same operations on the same
       // operands, so it is formed once and kept for the Lambert term.
@@ -949,45 +933,6 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
         const Col lc = intensify<FC>(intensify<FC>(Col{lt->col[0], lt->col[1], lt->col[2]}, inten), t);
         L = cadd<FC>(L, cmul<FC>(c, lc));
       }
-#else
-      for (int base = 0; base < S.n_lights; base += RT_LIGHT_GROUP) {
-        double tr[RT_LIGHT_GROUP];
-#pragma unroll
-        for (int k = 0; k < RT_LIGHT_GROUP; ++k) tr[k] = 0.0;
-        const int nk = S.n_lights - base < RT_LIGHT_GROUP ? S.n_lights - base : RT_LIGHT_GROUP;
-#pragma unroll 1
-        for (int k = 0; k < nk; ++k) {                                   // ONE traversal body in the code
-          const V3 lv = sub(ld3(S.lights[base + k].p), p);
-#ifdef RT_ABLATE_NO_SHADOWS
-          const double t = lv.x > 1e300 ? 0.5 : 1.0;
-#else
-          PROF_T0(p2);
-          const double t = shadow_transparency<SHARE, OBB>(S, p, normalized(lv), len(lv));   // :176-197
-          PROF_ADD(2, p2);
-#endif
-#pragma unroll
-          for (int j = 0; j < RT_LIGHT_GROUP; ++j) tr[j] = j == k ? t : tr[j];   // registers, no scratch
-        }
-        if (!have_shading) {
-          PROF_T0(p3);
-          shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
-          PROF_ADD(3, p3);
-          L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));                           // ambient (:172)
-          have_shading = true;
-        }
-#pragma unroll
-        for (int k = 0; k < RT_LIGHT_GROUP; ++k) {                       // :199-227
-          if (base + k >= S.n_lights || tr[k] == 0.0) continue;
-          cptr<RtLight> lt = &S.lights[base + k];
-          const V3 sdir = normalized(sub(ld3(lt->p), p));
-          double ang = rt_acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
-          if (ang >= PI_D / 2.0) ang = PI_D - ang;
-          const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
-          const Col lc = intensify<FC>(intensify<FC>(Col{lt->col[0], lt->col[1], lt->col[2]}, inten), tr[k]);
-          L = cadd<FC>(L, cmul<FC>(c, lc));
-        }
-      }
-#endif
       if (!have_shading) {
         shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
         L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));
@@ -1270,15 +1215,9 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
 #define RT_WAVES_PER_EU_NOREFR 5
 #endif
 #define RT_WAVES(REFR) ((REFR) ? RT_WAVES_PER_EU : RT_WAVES_PER_EU_NOREFR)
-// Workgroup = RT_WG_WX x RT_WG_WY waves of 8x8 pixels.
-#ifndef RT_WG_WX
-#define RT_WG_WX 1          // one wave per workgroup: measured 3-5% faster than 2x2 (r01q)
-#endif
-#ifndef RT_WG_WY
-#define RT_WG_WY 1
-#endif
-constexpr int RT_WG_THREADS = 64 * RT_WG_WX * RT_WG_WY;
-constexpr int RT_TILE_W = 8 * RT_WG_WX, RT_TILE_H = 8 * RT_WG_WY;
+// Workgroup = one wave of 8x8 pixels: measured 3-5 % faster than 2x2-wave workgroups (round 1).
+constexpr int RT_WG_THREADS = 64;
+constexpr int RT_TILE_W = 8, RT_TILE_H = 8;
 template <bool REFR, bool F64, bool CAL = false, bool FC = false>
 __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(RT_WAVES(REFR)))) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
                                                           int n_rows, int max_depth, uint8_t* __restrict__ out,
@@ -1288,7 +1227,7 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   __shared__ volatile char rt_pad[RT_DIAG_LDS];
   if (threadIdx.x == 0) rt_pad[0] = 0;
 #endif
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
   // Tile dispatch order (see launch_bands): `order` lists the tiles most expensive first, as
   // measured on a calibration launch that stored each tile's wave time in `cost`.
   // CAL (the calibration instantiation) is the only one that carries the timing code.
@@ -1297,8 +1236,8 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   if constexpr (CAL) t_start = wall_clock64();
   const unsigned tiles_x = (unsigned)(S.width + RT_TILE_W - 1) / RT_TILE_W;
   const int bx = (int)(tile % tiles_x), by = (int)(tile / tiles_x);
-  const int x = bx * RT_TILE_W + (wave % RT_WG_WX) * 8 + (lane & 7);
-  const int r = by * RT_TILE_H + (wave / RT_WG_WX) * 8 + (lane >> 3);
+  const int x = bx * RT_TILE_W + (lane & 7);
+  const int r = by * RT_TILE_H + (lane >> 3);
   if (x >= S.width || r >= n_rows) return;
   const int y = y_first + (r / band_rows) * band_pitch + r % band_rows;
   if (y >= S.height) return;
@@ -1307,8 +1246,8 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
 #if RT_LDS_FRAMES > 0
   constexpr int KLR = REFR ? RT_LDS_RFRAMES : 0;
-  __shared__ double s_frames[RT_WG_WX * RT_WG_WY][(RT_LDS_FRAMES * 4 + KLR * 7) * 64];   // frame stack, see trace()
-  lds_f64* lf = (lds_f64*)&s_frames[wave][lane];
+  __shared__ double s_frames[(RT_LDS_FRAMES * 4 + KLR * 7) * 64];   // frame stack, see trace()
+  lds_f64* lf = (lds_f64*)&s_frames[lane];
   const Col c = trace<REFR, NoRec, RT_LDS_FRAMES, FC, KLR>(make_ds(S), ro, rd, max_depth, nullptr, lf);
 #else
   const Col c = trace<REFR, NoRec, 0, FC>(make_ds(S), ro, rd, max_depth);
@@ -1718,6 +1657,9 @@ struct rt_ctx {
   int32_t max_depth = 10;
   int32_t kernel_opt = RT_KERNEL_AUTO;  // rt_ctx_set_option(RT_OPT_KERNEL)
   bool timing = true;                   // rt_ctx_set_option(RT_OPT_TIMING): launch events recorded
+  bool tile_order = true;               // rt_ctx_set_option(RT_OPT_TILE_ORDER): cost-ordered dispatch
+  bool fast_clamp = true;               // rt_ctx_set_option(RT_OPT_FAST_CLAMP): min/max clamps where exact
+  int n_cu = 256;                       // compute units of the device (wave slots = n_cu x 4 SIMDs x waves/SIMD)
   bool uploaded = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -1753,75 +1695,24 @@ using rt::fail;
     if (e_ != hipSuccess) return fail(RT_ERR_DEVICE, "%s failed: %s", #call, hipGetErrorString(e_)); \
   } while (0)
 
-#ifndef RT_ORDER_MODE_DEFAULT
-#define RT_ORDER_MODE_DEFAULT 0
-#endif
-#ifndef RT_ORDER_HEAVY_FRAC_DEFAULT
-#define RT_ORDER_HEAVY_FRAC_DEFAULT 0.1
-#endif
-#ifndef RT_ORDER_RUN
-#define RT_ORDER_RUN 1                // tiles per sorted run: 1 measured best (profiles/r01ah_tile_order_sweep.txt)
-#endif
-// RT_TILE_ORDER=0 in the environment turns the cost-ordered dispatch off (row-major tiles).
-static bool tile_order_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("RT_TILE_ORDER");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// Environment: RT_TILE_ORDER_DEBUG=1 prints each calibration's tile-cost statistics and the kernel
+// it picked to stderr (diagnostic).  Every tunable is a context option (rt_ctx_set_option).
 
-// Kernel choice for scenes without a transparent object (REFR = false).  RT_DEFERRED=1 in the
-// environment always takes the deferred-shadow kernel, RT_DEFERRED=0 never (the per-lane
-// megakernel, trace<false>).  By default:
-//   * launches of fewer than RT_ORDER_MIN_TILES tiles (fewer tiles than the chip has wave slots:
-//     latency-bound by definition) take the deferred kernel;
+// Kernel choice for scenes without a transparent object (REFR = false), RT_OPT_KERNEL AUTO:
+//   * launches of fewer than RT_ORDER_MIN_TILES tiles (no calibration) take the deferred kernel;
 //   * larger launches calibrate on the megakernel; the ordered launches that follow take the
 //     deferred kernel with split tiles when the launch has fewer than RT_DEFERRED_MAX_TILES tiles
-//     AND its costliest tile is longer than RT_TAIL_RATIO x the work per wave slot (sum of tile
-//     costs / 7168): then the tail, not the throughput, sets the time.
+//     AND its costliest tile is longer than the work per wave slot (sum of tile costs / the chip's
+//     wave slots for the calibrated kernel: CUs x 4 SIMDs x its waves per SIMD): then the tail,
+//     not the throughput, sets the time.
 // Same pixels either way.  Measured (profiles/r02h_inflight.txt, r02j_*): a rank's share of the
 // 4K globes frame at N = 8 / 4 (16320 / 32640 tiles, tail ratio 3.5 / 1.8) takes 0.146-0.178 /
 // 0.187-0.204 ms deferred + split against 0.244 / 0.254 ms in the megakernel, 1080p globes d5
 // (ratio 1.7) 0.219 against 0.26-0.28 ms; at N = 2 / 1 (64800 / 129600 tiles, ratio 1.0 / 0.5),
 // and for the 1080p single sphere (32400 tiles, ratio 0.75: no tail to speak of), the megakernel
-// is 7-20 % faster.
-#ifndef RT_DEFERRED_MAX_TILES
+// is 7-20 % faster.  The deferred kernel's order entries hold the tile index in 20 bits
+// (RT_SPLIT_TILE_MASK), so launches of more tiles always take the megakernel.
 #define RT_DEFERRED_MAX_TILES 40000
-#endif
-#ifndef RT_TAIL_RATIO
-#define RT_TAIL_RATIO 1.0
-#endif
-#ifndef RT_DEFERRED_DEFAULT
-#define RT_DEFERRED_DEFAULT (-1)
-#endif
-static int deferred_mode() {
-  static const int mode = [] {
-    const char* e = getenv("RT_DEFERRED");
-    return e ? (e[0] == '0' ? 0 : 1) : RT_DEFERRED_DEFAULT;
-  }();
-  return mode;
-}
-static size_t deferred_max_tiles() {
-  static const size_t v = [] {
-    const char* e = getenv("RT_DEFERRED_MAX_TILES");
-    return e ? (size_t)atoll(e) : (size_t)RT_DEFERRED_MAX_TILES;
-  }();
-  return v;
-}
-
-// RT_FAST_CLAMP=0 in the environment keeps the compare/select clamps even where the fast form is
-// exact (A/B timing; same pixels).
-#ifndef RT_FAST_CLAMP_DEFAULT
-#define RT_FAST_CLAMP_DEFAULT 1
-#endif
-static bool fast_clamp_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("RT_FAST_CLAMP");
-    return e ? e[0] != '0' : RT_FAST_CLAMP_DEFAULT != 0;
-  }();
-  return on;
-}
 
 static void drop_order(rt_ctx::OrderSlot& s) {
   if (s.d_order) (void)hipFree(s.d_order);     // hipFree waits for work that may still read it
@@ -1914,8 +1805,11 @@ int rt_ctx_create(int device, rt_ctx** out) {
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RT_ERR_DEVICE, "no HIP device available");
   if (device < 0 || device >= n) return fail(RT_ERR_INVALID, "device %d out of range (%d devices)", device, n);
   RT_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  RT_HIP(hipGetDeviceProperties(&prop, device));
   rt_ctx* c = new rt_ctx();
   c->device = device;
+  c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   memset(&c->dev, 0, sizeof c->dev);
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
     delete c;
@@ -2004,16 +1898,16 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   const size_t n_tiles = (size_t)tiles_x * (size_t)tiles_y;
   const int32_t key[7] = {a0, a1, a2, a3, max_depth, f64 ? 1 : 0, c->dev.width};
   const bool refr = c->dev.any_transparent != 0;
-  // Kernel choice for scenes without a transparent object (see deferred_mode): the per-lane
+  // Kernel choice for scenes without a transparent object (RT_DEFERRED_MAX_TILES): the per-lane
   // megakernel is fastest when the launch fills the GPU many times over (throughput-bound); a
   // launch bound by its costliest tiles' latency takes the deferred-shadow kernel with split
   // costly tiles (DESIGN.md "Deferred shadows").  An ordered launch takes its slot's choice.
-  const bool eligible = !refr && c->dev.n_lights <= RT_SH_TRCAP && RT_TILE_W == 8 && RT_TILE_H == 8;
-  // -1 auto, 0 megakernel, 1 deferred: the context's option, else the environment's default
-  const int dmode = c->kernel_opt == RT_KERNEL_MEGA ? 0 : c->kernel_opt == RT_KERNEL_DEFERRED ? 1 : deferred_mode();
+  const bool eligible = !refr && c->dev.n_lights <= RT_SH_TRCAP && n_tiles <= (size_t)RT_SPLIT_TILE_MASK + 1;
+  // -1 auto, 0 megakernel, 1 deferred (the context's RT_OPT_KERNEL)
+  const int dmode = c->kernel_opt == RT_KERNEL_MEGA ? 0 : c->kernel_opt == RT_KERNEL_DEFERRED ? 1 : -1;
   rt_ctx::OrderSlot* slot = nullptr;
   bool calibrate = false;
-  if (tile_order_enabled() && n_tiles >= RT_ORDER_MIN_TILES) {
+  if (c->tile_order && n_tiles >= RT_ORDER_MIN_TILES) {
     for (auto& s : c->order)
       if (s.valid && memcmp(s.key, key, sizeof(key)) == 0) slot = &s;
     if (!slot) {                      // calibrate into the empty or least recently used slot
@@ -2041,7 +1935,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   else if (dmode == 1) deferred = true;
   else if (order) deferred = slot->deferred;
   else if (calibrate) deferred = false;                       // calibrate on the megakernel
-  else deferred = n_tiles < RT_ORDER_MIN_TILES || (!tile_order_enabled() && n_tiles < deferred_max_tiles());
+  else deferred = n_tiles < RT_ORDER_MIN_TILES || (!c->tile_order && n_tiles < RT_DEFERRED_MAX_TILES);
   if (c->timing) RT_HIP(hipEventRecord(c->ev0, st));
 #define RT_LAUNCH_ROWS(R, F)                                                                                  \
   if (calibrate && fc) hipLaunchKernelGGL((render_rows_kernel<R, F, true, true>), grid, block, 0, st, c->dev, a0, a1, \
@@ -2061,7 +1955,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
                                   a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);                         \
   else hipLaunchKernelGGL((render_rows_deferred_kernel<F, false, false>), grid, dim3(64), 0, st, c->dev, a0, a1, a2, \
                           a3, max_depth, target, tstride, order, cost, rgbi);
-  const bool fc = c->dev.colour_fast != 0 && fast_clamp_enabled();
+  const bool fc = c->dev.colour_fast != 0 && c->fast_clamp;
   if (refr && f64) { RT_LAUNCH_ROWS(true, true) }
   else if (refr) { RT_LAUNCH_ROWS(true, false) }
   else if (deferred && f64) { RT_LAUNCH_DEFERRED(true) }
@@ -2078,55 +1972,28 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     std::vector<int32_t> h_order(n_tiles);
     RT_HIP(hipMemcpyAsync(h_cost.data(), slot->d_cost, n_tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     RT_HIP(hipStreamSynchronize(st));
-    // Longest-first: sort runs of RT_ORDER_RUN horizontally adjacent tiles (env RT_ORDER_RUN
-    // overrides) by their summed cost, each run's tiles kept consecutive.  With runs of 1 every
-    // tile is placed by its own cost; longer runs keep neighbours together (measured slower).
-    static const int run_env = [] { const char* e = getenv("RT_ORDER_RUN"); return e ? atoi(e) : 0; }();
-    const int run = run_env > 0 ? run_env : RT_ORDER_RUN, runs_x = (tiles_x + run - 1) / run;
-    const size_t n_runs = (size_t)runs_x * (size_t)tiles_y;
-    std::vector<uint64_t> run_cost(n_runs, 0);
-    std::vector<int32_t> run_order(n_runs);
-    for (size_t t = 0; t < n_tiles; ++t)
-      run_cost[(t / tiles_x) * runs_x + (t % tiles_x) / run] += h_cost[t];
-    for (size_t i = 0; i < n_runs; ++i) run_order[i] = (int32_t)i;
-    std::stable_sort(run_order.begin(), run_order.end(), [&](int32_t x, int32_t y) { return run_cost[x] > run_cost[y]; });
-    size_t k = 0;
-    for (int32_t rr : run_order) {
-      const int ty = rr / runs_x, tx0 = (rr % runs_x) * run;
-      for (int tx = tx0; tx < tx0 + run && tx < tiles_x; ++tx) h_order[k++] = ty * tiles_x + tx;
-    }
-    // Order mode (RT_ORDER_MODE; experiments): 0 = longest first; 1 = zigzag (costliest,
-    // cheapest, 2nd costliest, 2nd cheapest, ...); 2 = the costliest RT_ORDER_HEAVY_FRAC of the
-    // tiles longest first, then the rest row-major (spatially coherent, mixed costs).
-    static const int order_mode = [] { const char* e = getenv("RT_ORDER_MODE"); return e ? atoi(e) : RT_ORDER_MODE_DEFAULT; }();
-    static const double heavy_frac = [] { const char* e = getenv("RT_ORDER_HEAVY_FRAC"); return e ? atof(e) : RT_ORDER_HEAVY_FRAC_DEFAULT; }();
-    if (order_mode == 1) {
-      std::vector<int32_t> z(n_tiles);
-      for (size_t i = 0, a = 0, b = n_tiles; i < n_tiles; ++i) z[i] = (i & 1) ? h_order[--b] : h_order[a++];
-      h_order.swap(z);
-    } else if (order_mode == 2) {
-      const size_t nh = std::min(n_tiles, (size_t)(heavy_frac * (double)n_tiles));
-      std::sort(h_order.begin() + nh, h_order.end());
-    }
-    if (getenv("RT_TILE_ORDER_IDENTITY"))   // diagnostic: the table without the reordering
-      for (size_t i = 0; i < n_tiles; ++i) h_order[i] = (int32_t)i;
+    // Longest-first: every tile placed by its own measured cost (runs of 2-30 neighbouring tiles
+    // sorted together, zigzag and partly row-major orders measured 3-60 % slower,
+    // profiles/r01ah_tile_order_sweep.txt, r02k_order_ab.txt).
+    for (size_t i = 0; i < n_tiles; ++i) h_order[i] = (int32_t)i;
+    std::stable_sort(h_order.begin(), h_order.end(), [&](int32_t x, int32_t y) { return h_cost[x] > h_cost[y]; });
     bool tail_bound = false;
-    if (eligible && dmode == -1 && n_tiles < deferred_max_tiles()) {
+    // wave slots of the calibrated (mega)kernel on this device
+    const double slots = (double)c->n_cu * 4.0 * (double)RT_WAVES(refr);
+    if (eligible && dmode == -1 && n_tiles < RT_DEFERRED_MAX_TILES) {
       uint64_t sum = 0, mx = 0;
       for (uint32_t v : h_cost) { sum += v; mx = v > mx ? v : mx; }
-      static const double ratio = [] { const char* e = getenv("RT_TAIL_RATIO"); return e ? atof(e) : RT_TAIL_RATIO; }();
-      tail_bound = (double)mx > ratio * (double)sum / 7168.0;
+      tail_bound = (double)mx > (double)sum / slots;
     }
     slot->deferred = eligible && (dmode == 1 || tail_bound);
-    if (slot->deferred && n_tiles <= RT_SPLIT_TILE_MASK + 1) {
+    if (slot->deferred) {
       // Split the costliest tiles over P = 2, 4 or 8 waves (cost >= k * P * the median tile):
       // their shadow rays then spread over P x 64 lanes.  The factor k: 1 below 24000 tiles, 1.5
-      // above (env RT_SPLIT_K overrides both, 0 disables).  Swept at 1 / 1.25 / 1.5 / 2 / 3
+      // above.  Swept at 1 / 1.25 / 1.5 / 2 / 3
       // (profiles/r02bo_split_sweep.txt): the 4K N = 8 share (16320 tiles) 0.150 / 0.152 / 0.172 /
       // 0.170 / 0.183 ms; the N = 4 share (32400 tiles) 0.209 / 0.192 / 0.190 / 0.200 / 0.232 ms;
       // the whole 1080p d5 frame (32400 tiles) 0.208 / 0.189 / 0.184 / 0.181 / 0.225 ms.
-      static const double split_env = [] { const char* e = getenv("RT_SPLIT_K"); return e ? atof(e) : -1.0; }();
-      const double split_k = split_env >= 0.0 ? split_env : n_tiles < 24000 ? 1.0 : 1.5;
+      const double split_k = n_tiles < 24000 ? 1.0 : 1.5;
       std::vector<uint32_t> sorted_cost(h_cost);
       std::nth_element(sorted_cost.begin(), sorted_cost.begin() + n_tiles / 2, sorted_cost.end());
       const double med = std::max(1.0, (double)sorted_cost[n_tiles / 2]);
@@ -2135,7 +2002,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
       for (size_t i = 0; i < n_tiles; ++i) {
         const uint32_t t = (uint32_t)h_order[i];
         int lp = 0;
-        while (split_k > 0.0 && lp < RT_SPLIT_MAX_LOG2 && h_cost[t] >= split_k * med * (double)(2 << lp)) ++lp;
+        while (lp < RT_SPLIT_MAX_LOG2 && h_cost[t] >= split_k * med * (double)(2 << lp)) ++lp;
         for (int part = 0; part < (1 << lp); ++part)
           split.push_back((int32_t)(t | ((uint32_t)part << 20) | ((uint32_t)lp << 24)));
       }
@@ -2151,14 +2018,15 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     RT_HIP(hipMemcpyAsync(slot->d_order, h_order.data(), h_order.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
     RT_HIP(hipStreamSynchronize(st));
     slot->valid = true;
-    if (getenv("RT_TILE_ORDER_DEBUG")) {    // wave times in wall-clock ticks (100 MHz)
+    static const bool order_debug = getenv("RT_TILE_ORDER_DEBUG") != nullptr;
+    if (order_debug) {                      // wave times in wall-clock ticks (100 MHz)
       std::vector<uint32_t> v(h_cost);
       std::sort(v.begin(), v.end());
       double sum = 0.0;
       for (uint32_t x : v) sum += x;
-      fprintf(stderr, "tile order: %zu tiles, max %u, p99 %u, p90 %u, median %u, mean %.1f ticks; max / (sum / 7168) = %.3f; "
+      fprintf(stderr, "tile order: %zu tiles, max %u, p99 %u, p90 %u, median %u, mean %.1f ticks; max / (sum / %.0f slots) = %.3f; "
               "ordered launches: %s kernel, %u entries\n", n_tiles, v.back(), v[n_tiles * 99 / 100], v[n_tiles * 9 / 10],
-              v[n_tiles / 2], sum / n_tiles, v.back() / (sum / 7168.0), slot->deferred ? "deferred" : "mega", slot->grid);
+              v[n_tiles / 2], sum / n_tiles, slots, v.back() / (sum / slots), slot->deferred ? "deferred" : "mega", slot->grid);
     }
   }
   if (!dev_out) {
@@ -2320,7 +2188,7 @@ int rt_antialias(rt_ctx* c, const uint8_t* src_rgba8, size_t src_stride, double 
       if (n_req == 0) break;
       rays += n_req;
       const dim3 rg((n_req + 63) / 64);
-      const bool fc = c->dev.colour_fast != 0 && fast_clamp_enabled();
+      const bool fc = c->dev.colour_fast != 0 && c->fast_clamp;
 #define RT_LAUNCH_AA(R, F) hipLaunchKernelGGL((aa_trace_kernel<R, F>), rg, dim3(64), 0, st, c->dev, G, edges, req, n_req, (int)max_depth)
       if (c->dev.any_transparent && fc) RT_LAUNCH_AA(true, true);
       else if (c->dev.any_transparent) RT_LAUNCH_AA(true, false);
@@ -2479,6 +2347,17 @@ int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
     c->timed = false;                  // no launch recorded under the new setting yet
     return RT_OK;
   }
+  if (option == RT_OPT_TILE_ORDER || option == RT_OPT_FAST_CLAMP) {
+    if (value != 0 && value != 1) return fail(RT_ERR_INVALID, "option %d value %d", option, value);
+    if (option == RT_OPT_FAST_CLAMP) {
+      c->fast_clamp = value != 0;
+    } else if (c->tile_order != (value != 0)) {
+      RT_HIP(hipSetDevice(c->device));
+      drop_orders(c);
+      c->tile_order = value != 0;
+    }
+    return RT_OK;
+  }
   if (option != RT_OPT_KERNEL) return fail(RT_ERR_INVALID, "unknown option %d", option);
   if (value != RT_KERNEL_AUTO && value != RT_KERNEL_MEGA && value != RT_KERNEL_DEFERRED)
     return fail(RT_ERR_INVALID, "RT_OPT_KERNEL value %d", value);
@@ -2503,9 +2382,7 @@ int rt_stream_create(int device, void** stream) {
   std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0xFFFFFFFFu);
   if (prop.multiProcessorCount % 32) mask.back() = (1u << (prop.multiProcessorCount % 32)) - 1u;
   hipStream_t st = nullptr;
-  static const bool plain = getenv("RT_STREAM_PLAIN") != nullptr;   // diagnostic: a plain stream
-  if (plain) RT_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  else RT_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+  RT_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
   *stream = st;
   return RT_OK;
 }

@@ -285,6 +285,16 @@ class Renderer:
         render launch that last_kernel_ms() reads (each timed event costs the stream ~5 us)."""
         check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_TIMING, 1 if on else 0))
 
+    def set_tile_order(self, on: bool) -> None:
+        """rt_ctx_set_option(RT_OPT_TILE_ORDER): longest-first tile dispatch after a calibration launch
+        (default) or row-major tiles (same pixels)."""
+        check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_TILE_ORDER, 1 if on else 0))
+
+    def set_fast_clamp(self, on: bool) -> None:
+        """rt_ctx_set_option(RT_OPT_FAST_CLAMP): min/max colour clamps where the host proved them exact
+        (default) or the reference's compare/select clamps everywhere (same pixels)."""
+        check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_FAST_CLAMP, 1 if on else 0))
+
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()
         check(lib().rt_ctx_last_kernel_ms(self.h, ctypes.byref(ms)))
