@@ -92,6 +92,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0 = every core available to this process)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the extra phase after the timed region (N = 1: 4 frames in flight; N > 1: one "
+                         "frame at a time), which reports the other half of the scaling picture")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames whose renders may overlap, each on a stream with its own hardware queue "
                          "(0 = 1 at N = 1, so the roofline's kernel time and the rocprof trace are of one launch "
@@ -189,6 +192,34 @@ def load_pmc(config, world, layout):
 def load_traffic(config, world, layout):
     """HBM bytes per launch of the render kernel from the committed PMC summary (or None)."""
     return load_pmc(config, world, layout).get("hbm_bytes_per_launch")
+
+
+def issue_model(config, world, layout, kernel_ms, n_cu=256, clock_ghz=2.4):
+    """Where the render kernel's cycles go, from the committed PMC counters of this config
+    (profiles/pmc_summary.json) over THIS run's kernel time.  SIMD issue cycles per wave64 VALU
+    instruction: FP64 add/mul/fma 4 (16 lanes per cycle: the 78.6 TFLOP/s FP64 peak), FP64
+    transcendental (rcp/rsq/sqrt) 8, every other VALU instruction 2 (32 lanes per cycle, the f32
+    rate; MI355X_MICROARCH.md cycle constants).  valu_issue_fill = those cycles / (SIMDs x kernel
+    time x clock); wait_any_share = SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt);
+    valu_active_share = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES."""
+    c = load_pmc(config, world, layout).get("counters")
+    if not c or not kernel_ms or "SQ_INSTS_VALU" not in c:
+        return None
+    f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64"))
+    trans = c.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+    other = c["SQ_INSTS_VALU"] - f64 - trans
+    cyc = 4.0 * f64 + 8.0 * trans + 2.0 * other
+    avail = n_cu * 4 * kernel_ms * 1e-3 * clock_ghz * 1e9
+    out = {"valu_issue_fill": round(cyc / avail, 4), "valu_insts": c["SQ_INSTS_VALU"], "fp64_insts": f64,
+           "fp64_trans_insts": trans, "clock_ghz_assumed": clock_ghz,
+           "cycle_model": "FP64 add/mul/fma 4, FP64 trans 8, other VALU 2 SIMD cycles per wave64 instruction"}
+    if c.get("SQ_WAVE_CYCLES"):
+        out["wait_any_share"] = round(c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"], 4)
+        if "SQ_ACTIVE_INST_VALU" in c:
+            out["valu_active_share"] = round(c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"], 4)
+        if "SQ_WAIT_INST_ANY" in c:
+            out["wait_inst_share"] = round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+    return out
 
 
 def executed_fp64(config, world, layout, kernel_ms):
@@ -437,6 +468,20 @@ def main():
         rows_per_rank = counts
     busy_ms = mean_kernel_ms if K == 1 else elapsed * 1e3 / a.steps
 
+    # One definition of scaling (DESIGN.md "Multi-GPU"): the line carries BOTH the latency and the
+    # throughput figure at every N, measured after the timed region (they are not `value`):
+    # N = 1: `inflight4` -- the same frames with 4 in flight on own-queue streams (the N > 1 default);
+    # N > 1: `single_frame` -- one frame at a time, fully serialised, with events on the launch stream
+    #        around the rank's band render, the all-gather (as seen by the assembly: render end ->
+    #        gather done, so it includes waiting for the slowest rank) and the assembly kernel.
+    extra_steps = max(4, min(a.steps, 20))
+    single = infl = None
+    if multi and overlap and not a.no_extra:
+        single = single_frame_phase(a, rend, dist, D, stream, dev, slots[0], gath[0], frames[0], whole,
+                                    (y_first, band_rows, pitch, n_bands), H, W, world, layout, band, depth,
+                                    rehearse, extra_steps)
+    elif not multi and K == 1 and not a.no_extra:
+        infl = inflight_phase(T, rend, stream, dev, frames[0], whole, H, W, depth, local, 4, extra_steps)
     if rank == 0 and a.png:
         T.write_png(a.png, frames[(a.warmup + a.steps - 1) % nbuf].cpu().numpy())
 
@@ -498,6 +543,7 @@ def main():
             "frac_of_no_fma_ceiling": round(achieved / FP64_NO_FMA_TFLOPS, 4) if achieved else None,
             "no_fma_ceiling": FP64_NO_FMA_TFLOPS,
             "executed_fp64": executed_fp64(a.config, world, layout, busy_ms),
+            "issue": issue_model(a.config, world, layout, busy_ms),
         },
         "roofline_hbm": {
             "bound": "hbm",
@@ -523,6 +569,12 @@ def main():
                                "frames_in_flight": K, "gather": a.gather,
                                "kernel": "megakernel (rt_ctx_set_option)" if K >= 3 else "library's choice (auto)",
                                "frame_check": frame_check}
+    if single is not None:
+        line["single_frame"] = single
+        if line["value"] is not None and not rehearse:
+            single["value"] = round(W * H / (single["ms_per_step"] * 1e-3) / 1e6, 2)
+    if infl is not None:
+        line["inflight4"] = infl
     if world == 1 and not multi and not a.no_cpu_baseline:
         cb = cpu_baseline(text, W, H, t, depth, a.cpu_threads)
         cb["gpu_over_cpu"] = round(line["value"] / cb["value"], 1)
@@ -531,6 +583,79 @@ def main():
     json_out.flush()
     if multi:
         dist.destroy_process_group()
+
+
+def inflight_phase(T, rend, stream, dev, frame, whole, H, W, depth, local, K, steps):
+    """N = 1: `steps` frames with K in flight, each stream on a hardware queue of its own and writing
+    only its own buffer, the megakernel (as the N > 1 pipeline runs); checked against `whole`."""
+    import torch
+    hw = [T.HwStream(local) for _ in range(K)]
+    ss = [h.torch for h in hw]
+    bufs = [torch.zeros_like(frame) for _ in range(K)]
+    rend.set_kernel("mega")
+    rend.render_rows(0, H, max_depth=depth, out=bufs[0], stream=stream)      # calibrates this kernel's order
+    torch.cuda.synchronize(dev)
+    for i in range(2 * K):
+        rend.render_rows(0, H, max_depth=depth, out=bufs[i % K], stream=ss[i % K])
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        rend.render_rows(0, H, max_depth=depth, out=bufs[i % K], stream=ss[i % K])
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    bad = [b for b in range(K) if not torch.equal(bufs[b], whole)]
+    if bad:
+        raise SystemExit(f"inflight phase: frame buffer(s) {bad} differ from the single-launch render")
+    rend.set_kernel("auto")
+    for h in hw:
+        h.close()
+    return {"frames_in_flight": K, "steps": steps, "ms_per_step": round(el * 1e3 / steps, 4),
+            "value": round(W * H * steps / el / 1e6, 2), "kernel": "megakernel (rt_ctx_set_option)",
+            "frame_check": f"all {K} frame buffers == single-launch render",
+            "note": "throughput at the N > 1 default of 4 frames in flight: the N > 1 lines' `value` divides by this"}
+
+
+def single_frame_phase(a, rend, dist, D, stream, dev, slot, gath, frame, whole, geom, H, W, world, layout, band,
+                       depth, rehearse, steps):
+    """N > 1: one frame at a time, fully serialised (barrier + synchronize around every frame), the
+    library's kernel choice for a lone launch; events on the launch stream split each frame into
+    render / gather / assembly.  Returns the max over ranks of the mean per-step wall time and this
+    rank's event means (rank 0's in the line)."""
+    import torch
+    y_first, band_rows, pitch, n_bands = geom
+    rend.set_kernel("auto")
+    rec = []
+    warm = 3
+    for i in range(warm + steps):
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        t0 = time.perf_counter()
+        ev[0].record(stream)
+        rend.render_row_bands(y_first, band_rows, pitch, n_bands, slot, max_depth=depth, stream=stream)
+        ev[1].record(stream)
+        work = HostGather(gath, slot, stream) if rehearse else dist.all_gather_into_tensor(gath, slot, async_op=True)
+        work.wait()
+        ev[2].record(stream)
+        D.assemble(gath, H, world, layout, band, out=frame)
+        ev[3].record(stream)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        if i >= warm:
+            rec.append((dt, ev))
+    if not torch.equal(frame, whole):
+        raise SystemExit("single-frame phase: the assembled frame differs from the single-launch render")
+    wall = sum(d for d, _ in rec) / len(rec)
+    e = torch.tensor([wall], dtype=torch.float64, device="cpu" if rehearse else dev)
+    dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    mean = lambda i, j: sum(ev[i].elapsed_time(ev[j]) for _, ev in rec) / len(rec)
+    return {"frames_in_flight": 1, "steps": steps, "ms_per_step": round(float(e.item()) * 1e3, 4),
+            "render_ms": round(mean(0, 1), 4), "gather_ms": round(mean(1, 2), 4),
+            "assemble_ms": round(mean(2, 3), 4), "frame_ms": round(mean(0, 3), 4),
+            "kernel": "library's choice (auto) for a lone launch",
+            "basis": "wall time per serialised frame (max over ranks); render/gather/assemble: rank 0's events on "
+                     "its launch stream (gather = render end -> all-gather done, incl. waiting for the slowest rank)",
+            "frame_check": "assembled frame == single-launch render, on every rank"}
 
 
 class HostGather:
@@ -754,6 +879,8 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
             "executed_fp64": executed_fp64(a.config, 1, "contiguous",
                                            (sum(per_frame) / len(per_frame)) if K == 1 else elapsed * 1e3 / a.steps / len(mine)),
             "frac_of_no_fma_ceiling": round(achieved / FP64_NO_FMA_TFLOPS, 4) if achieved else None,
+            "issue": issue_model(a.config, 1, "contiguous",
+                                 (sum(per_frame) / len(per_frame)) if K == 1 else elapsed * 1e3 / a.steps / len(mine)),
         },
         "rays": rays_line(fl, F * W * H * a.steps / elapsed),
         "host_compile_upload_ms_per_frame": round(prep_ms, 3),

@@ -91,3 +91,23 @@ def test_shadow_walk_visits_likeliest_occluders_first():
         return [int(m.group(1)) for m in re.finditer(r"^strav \d+ obj=(-?\d+)", dump, re.M) if int(m.group(1)) >= 0]
     assert strav(_dump(open(os.path.join(SCENES, "globes.scene")).read())) == [4, 3, 1, 5, 2, 0]
     assert strav(_dump(open(os.path.join(SCENES, "spinning_globes.scene")).read(), 0.3)) == [0, 1, 2, 3]
+
+
+def _flags(dump: str) -> dict:
+    m = re.search(r"scene any_transparent=(\d) ray_chains=(\d) colour_fast=(\d) shadow_early_out=(\d)", dump)
+    assert m, dump[-2000:]
+    return dict(zip(("any_transparent", "ray_chains", "colour_fast", "shadow_early_out"), map(int, m.groups())))
+
+
+def test_ray_chain_flag():
+    """ray_chains (scene.cpp flatten): no object both transparent and reflective, so every hit spawns
+    at most one ray (raytracer.rs:242-267) and the refraction kernels may take the chain form."""
+    sg = _flags(_dump(open(os.path.join(SCENES, "spinning_globes.scene")).read(), 0.3))
+    assert sg["any_transparent"] == 1 and sg["ray_chains"] == 1          # glass refl 0, floor transp 0
+    fr = _flags(_dump(open(os.path.join(SCENES, "fractal.scene")).read()))
+    assert fr["any_transparent"] == 1 and fr["ray_chains"] == 0          # spheres refl 0.4, transp 0.6
+    gl = _flags(_dump(open(os.path.join(SCENES, "globes.scene")).read()))
+    assert gl["any_transparent"] == 0 and gl["ray_chains"] == 1
+    # -0 counts as zero, NaN as nonzero (IEEE comparisons, as the kernels test them)
+    assert _flags(_dump("draw(sphere(<0, 0, 0>, 30, red, 0 * (0 - 1), 0.5))"))["ray_chains"] == 1
+    assert _flags(_dump("draw(sphere(<0, 0, 0>, 30, red, 0.1, 0.5))"))["ray_chains"] == 0

@@ -830,7 +830,9 @@ typedef LDS_AS double lds_f64;
 // frame stack.  REFR = the scene has a transparent object (refraction frames need more state).
 // KL > 0: frames 0..KL-1 of the stack are in LDS at lf[(f * 4 + c) * 64] (lf = this lane's slot);
 // KLR > 0 (REFR): the pending-reflection state of frames 0..KLR-1 at lf[(KL * 4 + f * 7 + c) * 64].
-template <bool REFR, class Rec = NoRec, int KL = 0, bool FC = false, int KLR = 0>
+// CHAIN (REFR scenes with RtDevScene::ray_chains): every hit spawns at most one ray, so a refraction
+// frame never carries a pending reflection: frames are (A, w) as in the reflection-only kernels.
+template <bool REFR, class Rec = NoRec, int KL = 0, bool FC = false, int KLR = 0, bool CHAIN = false>
 __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, lds_f64* lf = nullptr) {
   double fA[RT_MAX_DEPTH_CAP][3];     // parent colour already intensified by (1 - w)
   double fW[RT_MAX_DEPTH_CAP];        // child weight w (transparency or reflectivity)
@@ -848,8 +850,9 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
       *A = {fA[f][0], fA[f][1], fA[f][2]}; *w = fW[f];
     }
   };
-  double fP[REFR ? RT_MAX_DEPTH_CAP : 1][3], fD[REFR ? RT_MAX_DEPTH_CAP : 1][3];
-  double fRP[REFR ? RT_MAX_DEPTH_CAP : 1];
+  constexpr bool TREE = REFR && !CHAIN;       // a hit may spawn two rays: pending reflections
+  double fP[TREE ? RT_MAX_DEPTH_CAP : 1][3], fD[TREE ? RT_MAX_DEPTH_CAP : 1][3];
+  double fRP[TREE ? RT_MAX_DEPTH_CAP : 1];
   uint32_t pend = 0;                  // bit f: frame f's reflection ray is still to be traced
   static_assert(RT_MAX_DEPTH_CAP <= 32, "pending-reflection bit mask");
   auto put_rframe = [&](int f, V3 P, V3 D, double rp) {
@@ -959,10 +962,10 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
       const bool do_refl = depth < max_depth && rp != 0.0 && (!inside || tir);   // :267
       if (do_refr && !tir) {
         put_frame(sp, intensify<FC>(L, 1.0 - transp), transp);
-        if constexpr (REFR) {
+        if constexpr (TREE) {
           pend = do_refl ? pend | (1u << sp) : pend & ~(1u << sp);
           if (do_refl) put_rframe(sp, p, reflect_dir(rd, n2), rp);
-        }
+        }                                                                  // CHAIN: do_refl is false here
         if constexpr (RECORD) { fSlot[sp] = slot; ray_type = 2; }        // TransmissionRay
         ++sp;
         ro = p;
@@ -971,7 +974,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
         descend = true;
       } else if (do_refl) {
         put_frame(sp, intensify<FC>(L, 1.0 - rp), rp);
-        if constexpr (REFR) pend &= ~(1u << sp);
+        if constexpr (TREE) pend &= ~(1u << sp);
         if constexpr (RECORD) { fSlot[sp] = slot; ray_type = 1; }        // ReflectionRay
         ++sp;
         rd = reflect_dir(rd, n2);
@@ -991,7 +994,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
       double fw;
       get_frame(f, &fa, &fw);
       const Col comb = cadd<FC>(fa, intensify<FC>(C, fw));
-      if constexpr (REFR) {
+      if constexpr (TREE) {
         if ((pend >> f) & 1u) {                                           // refraction done -> reflection
           pend &= ~(1u << f);
           double frp;
@@ -1206,23 +1209,34 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
 // runs that synchronised after every launch; with launches back to back (sustained clocks,
 // tools/ab_interleaved.py --burst) 5 is 1-3 % faster than 7 and cuts the launch's HBM traffic 9x
 // (2.30 -> 0.245 GB: the spills went to scratch), 6 is 5 % slower, 8 spills and is 1.7x slower
-// (profiles/r02o_waves_sustained.txt, r02q_ab.txt, r02r_ab.txt).  Refraction scenes keep 4
-// (128 VGPRs; 3 is equal, 5 is 1.5 % slower, profiles/r02s_ab.txt).
+// (profiles/r02o_waves_sustained.txt, r02q_ab.txt, r02r_ab.txt).  Refraction scenes with ray
+// trees keep 4 (128 VGPRs; 3 is equal, 5 is 1.5 % slower, profiles/r02s_ab.txt).
+// Kernel modes (RT_MODE_*): the reflection-only megakernel; refraction scenes whose rays form
+// chains (RtDevScene::ray_chains: frames are (A, w) only, no pending-reflection state); refraction
+// scenes with ray trees.
+#define RT_MODE_REFL 0
+#define RT_MODE_CHAIN 1
+#define RT_MODE_TREE 2
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 4
 #endif
 #ifndef RT_WAVES_PER_EU_NOREFR
 #define RT_WAVES_PER_EU_NOREFR 5
 #endif
+#ifndef RT_WAVES_PER_EU_CHAIN
+#define RT_WAVES_PER_EU_CHAIN 5
+#endif
 #define RT_WAVES(REFR) ((REFR) ? RT_WAVES_PER_EU : RT_WAVES_PER_EU_NOREFR)
+#define RT_WAVES_MODE(M) ((M) == RT_MODE_REFL ? RT_WAVES_PER_EU_NOREFR : (M) == RT_MODE_CHAIN ? RT_WAVES_PER_EU_CHAIN : RT_WAVES_PER_EU)
 // Workgroup = one wave of 8x8 pixels: measured 3-5 % faster than 2x2-wave workgroups (round 1).
 constexpr int RT_WG_THREADS = 64;
 constexpr int RT_TILE_W = 8, RT_TILE_H = 8;
-template <bool REFR, bool F64, bool CAL = false, bool FC = false>
-__global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(RT_WAVES(REFR)))) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
+template <int MODE, bool F64, bool CAL = false, bool FC = false>
+__global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(RT_WAVES_MODE(MODE)))) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
                                                           int n_rows, int max_depth, uint8_t* __restrict__ out,
                                                           size_t stride, const int32_t* __restrict__ order,
                                                           uint32_t* __restrict__ cost, int rgb) {
+  constexpr bool REFR = MODE != RT_MODE_REFL, CHAIN = MODE == RT_MODE_CHAIN;
 #ifdef RT_DIAG_LDS                       // diagnostic builds only: cap occupancy with an LDS pad
   __shared__ volatile char rt_pad[RT_DIAG_LDS];
   if (threadIdx.x == 0) rt_pad[0] = 0;
@@ -1245,12 +1259,12 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   PROF_T0(p5);
   camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
 #if RT_LDS_FRAMES > 0
-  constexpr int KLR = REFR ? RT_LDS_RFRAMES : 0;
+  constexpr int KLR = MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0;
   __shared__ double s_frames[(RT_LDS_FRAMES * 4 + KLR * 7) * 64];   // frame stack, see trace()
   lds_f64* lf = (lds_f64*)&s_frames[lane];
-  const Col c = trace<REFR, NoRec, RT_LDS_FRAMES, FC, KLR>(make_ds(S), ro, rd, max_depth, nullptr, lf);
+  const Col c = trace<REFR, NoRec, RT_LDS_FRAMES, FC, KLR, CHAIN>(make_ds(S), ro, rd, max_depth, nullptr, lf);
 #else
-  const Col c = trace<REFR, NoRec, 0, FC>(make_ds(S), ro, rd, max_depth);
+  const Col c = trace<REFR, NoRec, 0, FC, 0, CHAIN>(make_ds(S), ro, rd, max_depth);
 #endif
   PROF_ADD(5, p5);
   uint8_t* row = out + (size_t)r * stride;
@@ -1857,6 +1871,7 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   d.any_transparent = f.any_transparent;
   d.shadow_early_out = f.shadow_early_out;
   d.colour_fast = f.colour_fast;
+  d.ray_chains = f.ray_chains;
   d.cam = f.cam;
   c->max_depth = f.max_depth;
   c->uploaded = true;
@@ -1956,12 +1971,19 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   else hipLaunchKernelGGL((render_rows_deferred_kernel<F, false, false>), grid, dim3(64), 0, st, c->dev, a0, a1, a2, \
                           a3, max_depth, target, tstride, order, cost, rgbi);
   const bool fc = c->dev.colour_fast != 0 && c->fast_clamp;
-  if (refr && f64) { RT_LAUNCH_ROWS(true, true) }
-  else if (refr) { RT_LAUNCH_ROWS(true, false) }
+#ifdef RT_DIAG_NO_CHAIN                 // diagnostic A/B builds only: ray trees' kernel for chain scenes too
+  const bool chain = false;
+#else
+  const bool chain = refr && c->dev.ray_chains != 0;
+#endif
+  if (chain && f64) { RT_LAUNCH_ROWS(RT_MODE_CHAIN, true) }
+  else if (chain) { RT_LAUNCH_ROWS(RT_MODE_CHAIN, false) }
+  else if (refr && f64) { RT_LAUNCH_ROWS(RT_MODE_TREE, true) }
+  else if (refr) { RT_LAUNCH_ROWS(RT_MODE_TREE, false) }
   else if (deferred && f64) { RT_LAUNCH_DEFERRED(true) }
   else if (deferred) { RT_LAUNCH_DEFERRED(false) }
-  else if (f64) { RT_LAUNCH_ROWS(false, true) }
-  else { RT_LAUNCH_ROWS(false, false) }
+  else if (f64) { RT_LAUNCH_ROWS(RT_MODE_REFL, true) }
+  else { RT_LAUNCH_ROWS(RT_MODE_REFL, false) }
 #undef RT_LAUNCH_ROWS
 #undef RT_LAUNCH_DEFERRED
   RT_HIP(hipGetLastError());
@@ -1979,7 +2001,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     std::stable_sort(h_order.begin(), h_order.end(), [&](int32_t x, int32_t y) { return h_cost[x] > h_cost[y]; });
     bool tail_bound = false;
     // wave slots of the calibrated (mega)kernel on this device
-    const double slots = (double)c->n_cu * 4.0 * (double)RT_WAVES(refr);
+    const double slots = (double)c->n_cu * 4.0 * (double)(!refr ? RT_WAVES_PER_EU_NOREFR : c->dev.ray_chains ? RT_WAVES_PER_EU_CHAIN : RT_WAVES_PER_EU);
     if (eligible && dmode == -1 && n_tiles < RT_DEFERRED_MAX_TILES) {
       uint64_t sum = 0, mx = 0;
       for (uint32_t v : h_cost) { sum += v; mx = v > mx ? v : mx; }

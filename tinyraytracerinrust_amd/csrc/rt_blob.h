@@ -174,6 +174,6 @@ struct RtDevScene {
   int32_t any_transparent;          // some object has transparency != 0 (refraction possible)
   int32_t shadow_early_out;         // every transparency is finite: product==0 stays 0
   int32_t colour_fast;              // colour clamps may take the min/max form (render_kernels.hip FC)
-  int32_t pad1;
+  int32_t ray_chains;               // every hit spawns at most one ray (scene.cpp flatten)
   RtCamera cam;
 };

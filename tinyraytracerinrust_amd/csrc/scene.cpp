@@ -689,6 +689,12 @@ int flatten(const rt_scene& s, FlatScene* out) {
   // ambient term, the Lambert intensities (in [0, 1], 0 for NaN angles), the shadow products, the
   // weights 1 - w and w of every fold, and every clamped colour are all finite and >= +0.
   f.colour_fast = 1;
+  // ray_chains: a hit spawns a refraction ray only if transparency != 0 and not TIR, a reflection
+  // ray only if rp != 0 and (outside or TIR), rp = TIR ? refl + (1 - refl) * transp : refl
+  // (raytracer.rs:242-267).  When every object has transparency == 0 or reflectivity == 0 (IEEE
+  // comparisons: a NaN counts as nonzero), a refracted hit has rp = refl = +-0 (no reflection) and a
+  // TIR hit has no refraction: every hit spawns at most one ray, so each pixel's rays form a chain.
+  f.ray_chains = 1;
   auto nonneg = [](double x) { return std::isfinite(x) && !std::signbit(x); };
   auto unit = [&](double x) { return nonneg(x) && x <= 1.0; };
   for (const ObjectRec& o : s.objects) {
@@ -754,6 +760,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
     ob.transparency = m.transparency;
     ob.shadow_skip = m.transparency == 1.0;
     if (m.transparency != 0.0) f.any_transparent = 1;
+    if (m.transparency != 0.0 && m.reflectivity != 0.0) f.ray_chains = 0;
     if (!isfinite(m.transparency)) f.shadow_early_out = 0;
     if (!unit(m.reflectivity) || !unit(m.transparency)) f.colour_fast = 0;
     if (m.texture < 0 && !(nonneg(m.color[0]) && nonneg(m.color[1]) && nonneg(m.color[2]))) f.colour_fast = 0;
@@ -782,6 +789,8 @@ int flatten(const rt_scene& s, FlatScene* out) {
     while (off % 16) { f.texels.push_back(0); ++off; }
   }
   if (getenv("RT_DUMP_FLAT")) {                                // debugging aid: culling boxes
+    fprintf(stderr, "scene any_transparent=%d ray_chains=%d colour_fast=%d shadow_early_out=%d\n", f.any_transparent,
+            f.ray_chains, f.colour_fast, f.shadow_early_out);
     for (size_t i = 0; i < f.trav.size(); ++i)
       fprintf(stderr, "trav %zu obj=%d skip=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f]\n", i, f.trav[i].obj, f.trav[i].skip,
               f.trav[i].blo[0], f.trav[i].blo[1], f.trav[i].blo[2], f.trav[i].bhi[0], f.trav[i].bhi[1], f.trav[i].bhi[2]);

@@ -52,6 +52,7 @@ struct FlatScene {
   int32_t width, height, max_depth;
   int32_t any_transparent, shadow_early_out;
   int32_t colour_fast;   // every colour-op operand is finite and >= +0 (see flatten)
+  int32_t ray_chains;    // every hit spawns at most one ray: no object is both transparent and reflective
 };
 
 // Transformation math (transformation.rs:104-220), exact f64 op order.

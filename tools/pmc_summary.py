@@ -54,6 +54,11 @@ def main(tag="r01", config="globes4k", kernel="render_rows_kernel"):
             summ[f"{config}/n1/contiguous"]["executed_fp64_flops_per_launch"] = res["executed_fp64_flops_per_launch"]
         if "SQ_INSTS_VALU" in mean and "SQ_WAVES" in mean:
             summ[f"{config}/n1/contiguous"]["valu_insts_per_wave"] = round(mean["SQ_INSTS_VALU"] / mean["SQ_WAVES"], 1)
+        # the per-launch counters bench.py's roofline.issue block is derived from
+        keep = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                "SQ_INSTS_VALU_TRANS_F64", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+                "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE", "GRBM_COUNT")
+        summ[f"{config}/n1/contiguous"]["counters"] = {k: mean[k] for k in keep if k in mean}
         with open(summ_path, "w") as f:
             json.dump(summ, f, indent=1)
     print(json.dumps(res, indent=1))
