@@ -109,6 +109,8 @@ def parse():
                     help="anim120: frames dealt round-robin over this many HIP streams so independent "
                          "frames' kernels overlap (one 1080p frame does not fill the GPU to its end); "
                          "1 / 2 / 3 / 4 streams: 8226 / 8786 / 8901 / 8913 Mrays/s (profiles/r02cu_anim120_streams.txt)")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "mega", "deferred"],
+                    help="anim120: the renderers' RT_OPT_KERNEL (auto: the library's choice per launch)")
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="before the warmup steps, render untimed frames for this long so the GPU reaches its "
                          "sustained clocks (reported as `settle` in the line; 0 disables).  Measured: 20 steps after "
@@ -585,6 +587,9 @@ def main():
         dist.destroy_process_group()
 
 
+_KEEP = []
+
+
 def inflight_phase(T, rend, stream, dev, frame, whole, H, W, depth, local, K, steps):
     """N = 1: `steps` frames with K in flight, each stream on a hardware queue of its own and writing
     only its own buffer, the megakernel (as the N > 1 pipeline runs); checked against `whole`."""
@@ -607,8 +612,7 @@ def inflight_phase(T, rend, stream, dev, frame, whole, H, W, depth, local, K, st
     if bad:
         raise SystemExit(f"inflight phase: frame buffer(s) {bad} differ from the single-launch render")
     rend.set_kernel("auto")
-    for h in hw:
-        h.close()
+    _KEEP.extend(hw)             # the streams live until the process exits (as the main pipeline's)
     return {"frames_in_flight": K, "steps": steps, "ms_per_step": round(el * 1e3 / steps, 4),
             "value": round(W * H * steps / el / 1e6, 2), "kernel": "megakernel (rt_ctx_set_option)",
             "frame_check": f"all {K} frame buffers == single-launch render",
@@ -770,6 +774,7 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
         r = T.Renderer(local)
         r.upload(sc)
         r.set_timing(False)                               # bench's own events time the frames
+        r.set_kernel(a.kernel)
         rends.append(r)
     torch.cuda.synchronize(dev)
     prep_ms = (time.perf_counter() - t0) * 1e3 / max(1, len(mine))
@@ -861,6 +866,7 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
                         f"one step = the whole animation",
             "scene": f"{scene}.scene", "width": W, "height": H, "frames": F, "max_depth": depth,
             "parallelism": f"frames round-robin over {world} rank(s) (replicas), {K} HIP stream(s) per rank",
+            "kernel": a.kernel,
             "collective": None,
         },
         "roofline": {
@@ -870,7 +876,7 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
             "unit": "TFLOP/s",
             "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4) if achieved else None,
             "traffic": load_traffic(a.config, 1, "contiguous"),     # HBM bytes per frame (PMC, profiles/)
-            "kernel": "render_rows_kernel<REFR=true>",
+            "kernel": "render_rows_kernel<RT_MODE_CHAIN> or render_rows_deferred_kernel<REFR> (RT_OPT_KERNEL " + a.kernel + ")",
             "streams": K,
             "achieved_basis": "kernel event time" if K == 1 else "step wall time (frames overlap on the streams)",
             "kernel_ms_mean": round(sum(per_frame) / len(per_frame), 4),

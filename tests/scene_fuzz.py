@@ -31,9 +31,14 @@ def _colour(r, odd):
     return f"rgb({_num(r, 0, 1)}, {_num(r, 0, 1)}, {_num(r, 0, 1)})"
 
 
+_CHAINS = [False]      # random_scene(chains=True): no object both transparent and reflective
+
+
 def _material(r, odd, allow_transp=True):
     refl = r.choice([0, 0, 0.2, 0.5, 0.8] + ([1.3] if odd else []))
     transp = r.choice([0, 0, 0, 0.5, 0.9]) if allow_transp else 0
+    if _CHAINS[0] and transp != 0:
+        refl = 0                  # every hit spawns at most one ray (scene.cpp ray_chains)
     return f"{_colour(r, odd)}, {refl}, {transp}"
 
 
@@ -55,7 +60,17 @@ def _primitive(r, name):
     return f"{name} = cube({_vec(r, -15, 15)}, {_num(r, 4, 20)})"
 
 
-def random_scene(seed: int) -> str:
+def random_scene(seed: int, chains: bool = False) -> str:
+    """chains=True: transparent objects get reflectivity 0, so the scene's rays form chains (the
+    refraction chain kernels: render_kernels.hip RT_MODE_CHAIN and the deferred REFR path)."""
+    _CHAINS[0] = chains
+    try:
+        return _random_scene(seed)
+    finally:
+        _CHAINS[0] = False
+
+
+def _random_scene(seed: int) -> str:
     r = random.Random(seed)
     odd = r.random() < 0.3
     lines = []

@@ -12,7 +12,10 @@ pytestmark = pytest.mark.gpu
 
 CASES = [("globes", 0.0, 64, 48, 10), ("globes", 0.25, 161, 121, 10), ("globes", 0.0, 640, 480, 10),
          ("globes", 0.5, 640, 480, 3), ("three_cubes", 0.0, 160, 120, 10), ("spinning_cube", 0.3, 160, 120, 10),
-         ("ground_star", 0.2, 160, 120, 10), ("spinning_gimbals", 0.4, 160, 120, 10), ("fractal", 0.0, 96, 72, 10)]
+         ("ground_star", 0.2, 160, 120, 10), ("spinning_gimbals", 0.4, 160, 120, 10), ("fractal", 0.0, 96, 72, 10),
+         # refraction chains (glass shells of reflectivity 0): the deferred kernel's REFR path
+         ("spinning_globes", 0.3, 160, 120, 10), ("spinning_globes", 0.7, 640, 480, 10),
+         ("spinning_globes", 0.05, 640, 480, 4)]
 
 
 @pytest.mark.parametrize("name,t,W,H,d", CASES)

@@ -52,6 +52,41 @@ def test_random_scene_ordered_launches(T, seed):
     assert np.array_equal(frames[1], frames[2])
 
 
+@pytest.mark.parametrize("seed", range(3000, 3048))
+def test_random_chain_scene_small_frame(T, seed):
+    """Scenes whose transparent objects are not reflective (ray chains): small frames take the
+    deferred kernel's refraction-chain path (no calibration below 2048 tiles)."""
+    from oracle import oracle as O
+    text = random_scene(seed, chains=True)
+    W, H, d = 96, 72, 6
+    rt = T.RayTracer(W, H)
+    rt.max_depth = d
+    rt.load_scene(text, 0.0)
+    gu = rt.renderer.render_rows_host(0, H)
+    gf = rt.renderer.render_rows_host(0, H, f64=True)
+    rf, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H, f64=True)
+    assert_close(gu, gf, ru, rf, f"random chain scene {seed}")
+
+
+@pytest.mark.parametrize("seed", range(4000, 4012))
+@pytest.mark.parametrize("kernel", ["mega", "deferred", "auto"])
+def test_random_chain_scene_ordered_launches(T, seed, kernel):
+    """Ray-chain scenes at 512x384 (3072 tiles) through the calibration launch and the cost-ordered
+    launches: the refraction chain megakernel (RT_MODE_CHAIN) and the deferred kernel's REFR path with
+    its costliest tiles split over several waves."""
+    from oracle import oracle as O
+    text = random_scene(seed, chains=True)
+    W, H, d = 512, 384, 10
+    rt = T.RayTracer(W, H)
+    rt.max_depth = d
+    rt.load_scene(text, 0.0)
+    rt.renderer.set_kernel(kernel)
+    frames = [rt.renderer.render_rows_host(0, H) for _ in range(3)]
+    _, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H)
+    for k, f in enumerate(frames):
+        assert_close(f, None, ru, None, f"random chain scene {seed} {kernel}, launch {k}")
+
+
 @pytest.mark.parametrize("seed", range(2000, 2024))
 def test_random_scene_antialias(T, seed):
     """The adaptive anti-aliasing pass (rt_antialias, antialiaser.rs:87-191) on random scenes:

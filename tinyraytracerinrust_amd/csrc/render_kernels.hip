@@ -1054,9 +1054,16 @@ struct ShadowWin {                  // LDS, one per wave: 2.5 KB
 __device__ uint32_t g_tile_stats[RT_STATS_TILES][4];
 #endif
 
-template <int HC, bool FC = false>
+// REFR (scenes with RtDevScene::ray_chains and a transparent object): a hit spawns a refraction
+// ray (weight transparency) or, on TIR or for a reflective object, a reflection ray (weight rp,
+// raytracer.rs:261-265), never both, so the rays still form a chain and the same three phases
+// apply; the decisions, directions and weights are trace<true, ..., CHAIN>'s, the traversals take
+// the refraction kernels' template arguments (shared sphere terms, draw-order shadow walk: the
+// transparency product's order is the reference's).
+template <int HC, bool FC = false, bool REFR = false>
 __device__ Col trace_deferred(const DS& S, V3 ro, V3 rd, int max_depth, bool valid, ShadowWin* win,
                               [[maybe_unused]] int stats_tile = -1) {
+  constexpr bool SHARE = REFR && RT_SPHERE_SHARE, OBB = !REFR;
 #ifdef RT_TILE_STATS
   const uint64_t ts0 = wall_clock64();
   int rounds = 0;
@@ -1068,28 +1075,36 @@ __device__ Col trace_deferred(const DS& S, V3 ro, V3 rd, int max_depth, bool val
   if (valid) {
     for (int depth = 0;; ++depth) {
       double t_hit;
-      const int oi = nearest_hit(S, ro, rd, &t_hit, depth == 0 ? 0 : 1);
+      const int oi = nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit, depth == 0 ? 0 : 1);
       if (oi < 0) break;                                                   // BLACK (:152-160)
       const V3 p = add(ro, scale(rd, t_hit));                               // :162
       V3 nrm;
       Col c;
       double transp, refl;
       shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);                    // :163-170
-      // inside test (:230-235), exactly as trace(); no transparent object: no refraction, no TIR
-      bool inside = false;                                                 // needed only if a ray may spawn
-      if (depth < max_depth && refl != 0.0) {
+      // inside test (:230-235), exactly as trace(): needed only if a ray may spawn
+      bool inside = false;
+      if (depth < max_depth && (refl != 0.0 || (REFR && transp != 0.0))) {
         const V3 nd = scale(rd, -1.0);
         inside = inside_test(dot(nd, nrm) / (len(nd) * len(nrm)));
       }
-      const bool do_refl = depth < max_depth && refl != 0.0 && !inside;    // :267
+      const V3 n2 = inside ? scale(nrm, -1.0) : nrm;
+      bool tir = false;
+      V3 tdir = {0.0, 0.0, 0.0};
+      const bool do_refr = REFR && depth < max_depth && transp != 0.0;     // :242
+      const double r1 = inside ? 1.45 : 1.0, r2 = inside ? 1.0 : 1.45;
+      if (do_refr) tdir = refract_dir(rd, n2, r1 / r2, &tir);
+      const double rp = tir ? refl + (1.0 - refl) * transp : refl;         // :261-265
+      const bool refracts = do_refr && !tir;
+      const bool do_refl = !refracts && depth < max_depth && rp != 0.0 && (!inside || tir);   // :267
       hP[nh][0] = p.x; hP[nh][1] = p.y; hP[nh][2] = p.z;
       hN[nh][0] = nrm.x; hN[nh][1] = nrm.y; hN[nh][2] = nrm.z;
       hC[nh][0] = c.r; hC[nh][1] = c.g; hC[nh][2] = c.b;
-      hW[nh] = refl;
+      hW[nh] = refracts ? transp : rp;
       ++nh;
-      last_spawned = do_refl;
-      if (!do_refl) break;
-      rd = reflect_dir(rd, nrm);                                            // !inside: n2 = n
+      last_spawned = refracts || do_refl;
+      if (!last_spawned) break;
+      rd = refracts ? tdir : reflect_dir(rd, n2);
       ro = p;
     }
   }
@@ -1129,7 +1144,7 @@ __device__ Col trace_deferred(const DS& S, V3 ro, V3 rd, int max_depth, bool val
       const int h = j % n_pub, k = j / n_pub;
       const V3 p = {win->px[h], win->py[h], win->pz[h]};
       const V3 lv = sub(ld3(S.lights[k].p), p);
-      win->tr[j] = shadow_transparency(S, p, normalized(lv), len(lv));
+      win->tr[j] = shadow_transparency<SHARE, OBB, OBB>(S, p, normalized(lv), len(lv));
     }
     __syncthreads();
     for (int i = 0; i < take; ++i) {                                        // L_h in light order
@@ -1294,7 +1309,7 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
 #ifndef RT_WAVES_PER_EU_DEFERRED
 #define RT_WAVES_PER_EU_DEFERRED 7
 #endif
-template <bool F64, bool CAL = false, bool FC = false>
+template <bool F64, bool CAL = false, bool FC = false, bool REFR = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_DEFERRED))) void
 render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth,
                             uint8_t* __restrict__ out, size_t stride, const int32_t* __restrict__ order,
@@ -1318,7 +1333,7 @@ render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_p
   }
   V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
   if (valid) camera_ray(S.cam, (double)x, (double)y, &ro, &rd);             // get_pixel(x as f64, y as f64)
-  const Col c = trace_deferred<RT_MAX_DEPTH_CAP + 1, FC>(make_ds(S), ro, rd, max_depth, valid, &win, CAL ? (int)tile : -1);
+  const Col c = trace_deferred<RT_MAX_DEPTH_CAP + 1, FC, REFR>(make_ds(S), ro, rd, max_depth, valid, &win, CAL ? (int)tile : -1);
   if (valid) {
     uint8_t* row = out + (size_t)r * stride;
     if constexpr (F64) {
@@ -1917,7 +1932,13 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   // megakernel is fastest when the launch fills the GPU many times over (throughput-bound); a
   // launch bound by its costliest tiles' latency takes the deferred-shadow kernel with split
   // costly tiles (DESIGN.md "Deferred shadows").  An ordered launch takes its slot's choice.
-  const bool eligible = !refr && c->dev.n_lights <= RT_SH_TRCAP && n_tiles <= (size_t)RT_SPLIT_TILE_MASK + 1;
+#ifdef RT_DIAG_NO_CHAIN                 // diagnostic A/B builds only: ray trees' kernel for chain scenes too
+  const bool chain = false;
+#else
+  const bool chain = refr && c->dev.ray_chains != 0;
+#endif
+  // the deferred kernel takes scenes whose rays form chains (reflection-only, or refraction chains)
+  const bool eligible = (!refr || chain) && c->dev.n_lights <= RT_SH_TRCAP && n_tiles <= (size_t)RT_SPLIT_TILE_MASK + 1;
   // -1 auto, 0 megakernel, 1 deferred (the context's RT_OPT_KERNEL)
   const int dmode = c->kernel_opt == RT_KERNEL_MEGA ? 0 : c->kernel_opt == RT_KERNEL_DEFERRED ? 1 : -1;
   rt_ctx::OrderSlot* slot = nullptr;
@@ -1961,27 +1982,24 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
                                   max_depth, target, tstride, order, cost, rgbi);                                       \
   else hipLaunchKernelGGL((render_rows_kernel<R, F, false, false>), grid, block, 0, st, c->dev, a0, a1, a2, a3,   \
                           max_depth, target, tstride, order, cost, rgbi);
-#define RT_LAUNCH_DEFERRED(F)                                                                                   \
-  if (calibrate && fc) hipLaunchKernelGGL((render_rows_deferred_kernel<F, true, true>), grid, dim3(64), 0, st, c->dev, \
-                                          a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);             \
-  else if (calibrate) hipLaunchKernelGGL((render_rows_deferred_kernel<F, true, false>), grid, dim3(64), 0, st, c->dev, \
-                                         a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);              \
-  else if (fc) hipLaunchKernelGGL((render_rows_deferred_kernel<F, false, true>), grid, dim3(64), 0, st, c->dev, a0, \
-                                  a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);                         \
-  else hipLaunchKernelGGL((render_rows_deferred_kernel<F, false, false>), grid, dim3(64), 0, st, c->dev, a0, a1, a2, \
-                          a3, max_depth, target, tstride, order, cost, rgbi);
+#define RT_LAUNCH_DEFERRED(F, R)                                                                                \
+  if (calibrate && fc) hipLaunchKernelGGL((render_rows_deferred_kernel<F, true, true, R>), grid, dim3(64), 0, st,    \
+                                          c->dev, a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);     \
+  else if (calibrate) hipLaunchKernelGGL((render_rows_deferred_kernel<F, true, false, R>), grid, dim3(64), 0, st,    \
+                                         c->dev, a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);      \
+  else if (fc) hipLaunchKernelGGL((render_rows_deferred_kernel<F, false, true, R>), grid, dim3(64), 0, st, c->dev,   \
+                                  a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);                     \
+  else hipLaunchKernelGGL((render_rows_deferred_kernel<F, false, false, R>), grid, dim3(64), 0, st, c->dev, a0, a1,  \
+                          a2, a3, max_depth, target, tstride, order, cost, rgbi);
   const bool fc = c->dev.colour_fast != 0 && c->fast_clamp;
-#ifdef RT_DIAG_NO_CHAIN                 // diagnostic A/B builds only: ray trees' kernel for chain scenes too
-  const bool chain = false;
-#else
-  const bool chain = refr && c->dev.ray_chains != 0;
-#endif
-  if (chain && f64) { RT_LAUNCH_ROWS(RT_MODE_CHAIN, true) }
+  if (deferred && chain && f64) { RT_LAUNCH_DEFERRED(true, true) }
+  else if (deferred && chain) { RT_LAUNCH_DEFERRED(false, true) }
+  else if (chain && f64) { RT_LAUNCH_ROWS(RT_MODE_CHAIN, true) }
   else if (chain) { RT_LAUNCH_ROWS(RT_MODE_CHAIN, false) }
   else if (refr && f64) { RT_LAUNCH_ROWS(RT_MODE_TREE, true) }
   else if (refr) { RT_LAUNCH_ROWS(RT_MODE_TREE, false) }
-  else if (deferred && f64) { RT_LAUNCH_DEFERRED(true) }
-  else if (deferred) { RT_LAUNCH_DEFERRED(false) }
+  else if (deferred && f64) { RT_LAUNCH_DEFERRED(true, false) }
+  else if (deferred) { RT_LAUNCH_DEFERRED(false, false) }
   else if (f64) { RT_LAUNCH_ROWS(RT_MODE_REFL, true) }
   else { RT_LAUNCH_ROWS(RT_MODE_REFL, false) }
 #undef RT_LAUNCH_ROWS

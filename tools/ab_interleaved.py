@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--upload-env", nargs="*", default=[],
                     help="per library (in order): KEY=VAL set in the environment while its scene is compiled and "
                          "uploaded (host-side flattening switches, e.g. RT_NO_LIT_ORDER=1); '-' for none")
+    ap.add_argument("--kernel", nargs="*", default=[],
+                    help="per library (in order): RT_OPT_KERNEL auto / mega / deferred for its context; '-' keeps auto. "
+                         "A library path may repeat with different kernels")
     a = ap.parse_args()
     import torch
     W, H = (int(v) for v in a.size.split("x"))
@@ -49,7 +52,10 @@ def main():
         assert L.rt_ctx_upload(cx, sc) == 0
         if env:
             del os.environ[env.split("=", 1)[0]]
-        ctxs.append((path + (f" [{env}]" if env else ""), L, cx, []))
+        kern = a.kernel[li] if li < len(a.kernel) and a.kernel[li] != "-" else None
+        if kern:
+            assert L.rt_ctx_set_option(cx, 0, {"auto": 0, "mega": 1, "deferred": 2}[kern]) == 0
+        ctxs.append((path + (f" [{env}]" if env else "") + (f" <{kern}>" if kern else ""), L, cx, []))
     import time
     for rep in range(a.reps + 3):
         for path, L, cx, ms in ctxs:
