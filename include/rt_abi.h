@@ -234,7 +234,9 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  *     tiles split over several waves, every other launch the per-lane megakernel;
  *   RT_KERNEL_MEGA: always the megakernel -- best when several frames are in flight on different
  *     streams (their launches overlap, so no launch's tail leaves the GPU idle);
- *   RT_KERNEL_DEFERRED: always the deferred-shadow kernel.
+ *   RT_KERNEL_DEFERRED: always the deferred-shadow kernel (scenes whose rays form chains);
+ *   RT_KERNEL_WAVEFRONT: the launch-wide wavefront path for any scene: one pass per recursion depth
+ *     over a dense queue of that depth's rays, then a bottom-up fold (render_kernels.hip wf_*).
  * Changing the kernel drops the context's tile orders (the next launch of each geometry
  * calibrates again).  Scenes with a transparent object always take the refraction megakernel.
  * RT_OPT_TIMING: 1 (default) records a HIP event pair around every render launch for
@@ -245,9 +247,16 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  * calibration launch (a host synchronisation per new geometry); 0 dispatches row-major.
  * RT_OPT_FAST_CLAMP: 1 (default) lets the kernels clamp colours with min/max where the host proved
  * it bit-identical to the reference's compare/select clamp (RtDevScene::colour_fast); 0 keeps the
- * compare/select form everywhere (A/B checks). */
-typedef enum rt_option { RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3 } rt_option;
-typedef enum rt_kernel_choice { RT_KERNEL_AUTO = 0, RT_KERNEL_MEGA = 1, RT_KERNEL_DEFERRED = 2 } rt_kernel_choice;
+ * compare/select form everywhere (A/B checks).
+ * RT_OPT_WAVEFRONT_CAP: rays each recursion level of the wavefront path holds, in percent of the
+ * launch's pixel slots (1..400, default 200); a pixel whose ray tree overflows a level is rendered
+ * again by the per-lane megakernel (same bits), so the value trades memory against that fallback. */
+typedef enum rt_option {
+  RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4
+} rt_option;
+typedef enum rt_kernel_choice {
+  RT_KERNEL_AUTO = 0, RT_KERNEL_MEGA = 1, RT_KERNEL_DEFERRED = 2, RT_KERNEL_WAVEFRONT = 3
+} rt_kernel_choice;
 int rt_ctx_set_option(rt_ctx* ctx, int32_t option, int32_t value);
 void rt_ctx_free(rt_ctx* ctx);
 /* A HIP stream on a hardware queue of its own (hipExtStreamCreateWithCUMask with every CU

@@ -1,0 +1,97 @@
+"""The launch-wide wavefront path (render_kernels.hip wf_trace_kernel / wf_fold_kernel /
+wf_fixup_kernel; rt_ctx_set_option(RT_OPT_KERNEL, RT_KERNEL_WAVEFRONT)): one pass per recursion
+depth over a dense queue of that depth's rays, then the bottom-up fold of raytracer.rs:256-279.
+Every frame against the oracle (src/raytracer/raytracer.rs:132-287): reflection chains, refraction
+chains, ray trees (fractal.scene's glass spheres are transparent AND reflective), row bands as the
+multi-GPU ranks render them, and pixels whose trees overflow a level (RT_OPT_WAVEFRONT_CAP at 1 %:
+the fix-up kernel re-renders them)."""
+import numpy as np
+import pytest
+
+from tests.conftest import SCENES, scene_text
+from tests.test_gpu_parity import assert_close
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("globes", 0.0, 160, 120, 10), ("globes", 0.25, 640, 480, 10), ("globes", 0.0, 320, 240, 3),
+         ("spinning_globes", 0.3, 320, 240, 10), ("spinning_globes", 0.7, 160, 120, 4),
+         ("three_cubes", 0.0, 160, 120, 10), ("spinning_cube", 0.3, 160, 120, 10), ("ground_star", 0.2, 160, 120, 10),
+         ("spinning_gimbals", 0.4, 160, 120, 10), ("fractal", 0.0, 160, 120, 10), ("fractal", 0.0, 96, 72, 2)]
+
+
+def _render(text, t, W, H, d, cap=None, rows=None):
+    import tinyraytracerinrust_amd as T
+    rt = T.RayTracer(W, H)
+    rt.max_depth = d
+    rt.load_scene(text, t, asset_dir=SCENES)
+    r = rt.renderer
+    r.set_kernel("wavefront")
+    if cap is not None:
+        r.set_wavefront_cap(cap)
+    y0, y1 = rows or (0, H)
+    return r.render_rows_host(y0, y1), r.render_rows_host(y0, y1, f64=True)
+
+
+@pytest.mark.parametrize("name,t,W,H,d", CASES)
+def test_wavefront_parity(worldmap, name, t, W, H, d):
+    from oracle import oracle as O
+    gu, gf = _render(scene_text(name), t, W, H, d)
+    rf, ru = O.OracleScene(scene_text(name), t, W, H, max_depth=d).render(0, H, f64=True)
+    assert_close(gu, gf, ru, rf, f"wavefront {name} t={t} {W}x{H} d={d}")
+
+
+@pytest.mark.parametrize("name,t", [("fractal", 0.0), ("spinning_globes", 0.3), ("globes", 0.0)])
+def test_wavefront_level_overflow_fixup(worldmap, name, t):
+    """Levels of 1 % of the pixel slots: most trees overflow, and their pixels come from the fix-up."""
+    from oracle import oracle as O
+    W, H, d = 128, 96, 10
+    gu, gf = _render(scene_text(name), t, W, H, d, cap=1)
+    rf, ru = O.OracleScene(scene_text(name), t, W, H, max_depth=d).render(0, H, f64=True)
+    assert_close(gu, gf, ru, rf, f"wavefront overflow {name}")
+
+
+def test_wavefront_rows_and_bands(worldmap):
+    """Row ranges and cyclic row bands (a multi-GPU rank's share) through the wavefront path."""
+    import torch
+    import tinyraytracerinrust_amd as T
+    from tinyraytracerinrust_amd import distributed as D
+    from oracle import oracle as O
+    W, H = 200, 150
+    text = scene_text("fractal")
+    ref_f, ref_u8 = O.OracleScene(text, 0.0, W, H).render(0, H, f64=True)
+    gu, gf = _render(text, 0.0, W, H, 10, rows=(17, 131))
+    assert_close(gu, gf, ref_u8[17:131], ref_f[17:131], "wavefront rows 17..131")
+    rt = T.RayTracer(W, H)
+    rt.load_scene(text, 0.0, asset_dir=SCENES)
+    r = rt.renderer
+    r.set_kernel("wavefront")
+    world, band = 3, 8
+    slot_rows = D.rows_per_rank(H, world, "cyclic", band)
+    gath = torch.zeros((world * slot_rows, W, 4), dtype=torch.uint8, device="cuda")
+    for rank in range(world):
+        y_first, band_rows, pitch, n_bands = D.band_params(H, world, rank, "cyclic", band)
+        r.render_row_bands(y_first, band_rows, pitch, n_bands, gath[rank * slot_rows:(rank + 1) * slot_rows])
+    frame = D.assemble(gath, H, world, "cyclic", band)
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy(), ref_u8)
+
+
+@pytest.mark.parametrize("seed", range(5000, 5032))
+def test_wavefront_random_scenes(seed):
+    """Seeded random scenes (trees and chains, odd materials) through the wavefront path."""
+    from tests.scene_fuzz import random_scene
+    from oracle import oracle as O
+    text = random_scene(seed, chains=seed % 2 == 1)
+    W, H, d = 96, 72, 6
+    gu, gf = _render(text, 0.0, W, H, d)
+    rf, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H, f64=True)
+    assert_close(gu, gf, ru, rf, f"wavefront random scene {seed}")
+
+
+def test_wavefront_option_bounds():
+    import tinyraytracerinrust_amd as T
+    rt = T.RayTracer(64, 48)
+    rt.load_scene("draw(sphere(<0, 0, 0>, 30, red))", 0.0)
+    for bad in (0, 401):
+        with pytest.raises(T.RtError):
+            rt.renderer.set_wavefront_cap(bad)

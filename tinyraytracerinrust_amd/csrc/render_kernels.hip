@@ -1350,6 +1350,258 @@ render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_p
     if (lane == 0) cost[tile] = (uint32_t)(wall_clock64() - t_start);
 }
 
+// ====================================================================== wavefront path
+// get_ray_color (raytracer.rs:132-287) launch-wide, one bounce level per pass: level d holds every
+// ray of recursion depth d of the launch, densely, one lane per ray.  Per level:
+//   wf_trace_kernel  nearest hit, shadow rays, shading, the inside / refraction / TIR / reflection
+//                    decisions of trace() (the same operations in the same order); the rays a hit
+//                    spawns are appended to level d + 1 (one ballot + one atomic per wave: a wave's
+//                    refraction children, then its reflection children, keep their lanes' order), the
+//                    hit record (L, the two weights, the children's slots) stays at its slot;
+//   wf_fold_kernel   after every level is traced, from the deepest level up: a ray's colour from its
+//                    hit record and its children's colours (already folded into their L slots):
+//                      refraction child: comb = in_range(L.intensify(1 - t) + C_t.intensify(t)),
+//                      then a reflection child: in_range(comb.intensify(1 - rp) + C_r.intensify(rp)),
+//                    exactly the post-order of raytracer.rs:256-279 (trace()'s frame fold).  Level 0's
+//                    fold writes the pixels.
+// Lanes whose pixel's tree ended early no longer idle in its wave (the megakernel's per-lane tree
+// walk keeps a wave alive for its deepest tree): every pass starts with every lane on a live ray.
+// Levels >= 1 hold up to 2 x the launch's pixel slots; a ray that finds its level full marks its
+// pixel, and wf_fixup_kernel re-renders marked pixels with trace() (same bits, rarely taken).
+struct WfArena {
+  uint8_t* base;          // level tables (wf_level)
+  uint32_t* count;        // count[d]: rays appended to level d (d >= 1); count[RT_MAX_DEPTH_CAP + 2]: any overflow
+  uint8_t* ovf;           // per pixel slot: its tree overflowed a level
+  uint32_t slots, cap;    // level 0 = the pixel slots (8x8 tiles x 64), levels >= 1: cap rays each
+};
+struct WfLevel {
+  double *ox, *oy, *oz, *dx, *dy, *dz;   // levels >= 1: the ray
+  double *Lr, *Lg, *Lb, *wt, *wr;        // hit record: L (then the folded colour), refraction / reflection weights
+  int32_t *pix, *ct, *cr;                // pixel slot (levels >= 1), children's slots in level d + 1 (-1: none)
+};
+constexpr size_t RT_WF_BYTES0 = 5 * 8 + 2 * 4, RT_WF_BYTES = 11 * 8 + 3 * 4;
+__device__ __forceinline__ WfLevel wf_level(const WfArena& A, int d) {
+  WfLevel v;
+  const size_t len = d == 0 ? A.slots : A.cap;
+  double* f = (double*)(A.base + (d == 0 ? 0 : (size_t)A.slots * RT_WF_BYTES0 + (size_t)(d - 1) * A.cap * RT_WF_BYTES));
+  if (d == 0) {
+    v.ox = v.oy = v.oz = v.dx = v.dy = v.dz = nullptr;
+    v.Lr = f; v.Lg = f + len; v.Lb = f + 2 * len; v.wt = f + 3 * len; v.wr = f + 4 * len;
+    int32_t* q = (int32_t*)(f + 5 * len);
+    v.pix = nullptr; v.ct = q; v.cr = q + len;
+  } else {
+    v.ox = f; v.oy = f + len; v.oz = f + 2 * len; v.dx = f + 3 * len; v.dy = f + 4 * len; v.dz = f + 5 * len;
+    v.Lr = f + 6 * len; v.Lg = f + 7 * len; v.Lb = f + 8 * len; v.wt = f + 9 * len; v.wr = f + 10 * len;
+    int32_t* q = (int32_t*)(f + 11 * len);
+    v.pix = q; v.ct = q + len; v.cr = q + 2 * len;
+  }
+  return v;
+}
+// pixel slot -> (x, output row r); false outside the launch's rows / frame
+__device__ __forceinline__ bool wf_pixel(const RtDevScene& S, uint32_t slot, int y_first, int band_rows, int band_pitch,
+                                         int n_rows, int* x, int* r, int* y) {
+  const unsigned tiles_x = (unsigned)(S.width + 7) / 8, tile = slot >> 6, l = slot & 63;
+  *x = (int)(tile % tiles_x) * 8 + (int)(l & 7);
+  *r = (int)(tile / tiles_x) * 8 + (int)(l >> 3);
+  if (*x >= S.width || *r >= n_rows) return false;
+  *y = y_first + (*r / band_rows) * band_pitch + *r % band_rows;
+  return *y < S.height;
+}
+
+// One ray of trace()'s loop body: nearest hit, the light loop (shadow rays first, then the shading
+// inputs), the inside test and the refraction / reflection decisions (raytracer.rs:141-280).
+template <bool REFR, bool FC>
+__device__ __forceinline__ void wf_ray(const DS& S, V3 ro, V3 rd, int depth, int max_depth, Col* Lo, double* wt,
+                                       double* wr, bool* ch_t, bool* ch_r, V3* po, V3* dt, V3* dr) {
+  constexpr bool SHARE = REFR && RT_SPHERE_SHARE, OBB = !REFR;
+  *ch_t = *ch_r = false;
+  *Lo = {0.0, 0.0, 0.0};
+  *wt = *wr = 0.0;
+  double t_hit;
+  const int oi = nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit, depth == 0 ? 0 : 1);
+  if (oi < 0) return;                                                   // Color::BLACK (:152-160)
+  const V3 p = add(ro, scale(rd, t_hit));                               // :162
+  V3 nrm = {0.0, 0.0, 0.0};
+  Col c = {0.0, 0.0, 0.0}, L = {0.0, 0.0, 0.0};
+  double transp = 0.0, refl = 0.0;
+  bool have_shading = false;
+#pragma unroll 1
+  for (int k = 0; k < S.n_lights; ++k) {                                // :175-228, as trace()
+    cptr<RtLight> lt = &S.lights[k];
+    const V3 lv = sub(ld3(lt->p), p);
+    double ll, ill;
+    len_inv(lv, &ll, &ill);
+    const V3 sdir = scale(lv, ill);
+    const double t = shadow_transparency<SHARE, OBB>(S, p, sdir, ll);
+    if (!have_shading) {
+      shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
+      L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));
+      have_shading = true;
+    }
+    if (t == 0.0) continue;
+    double ang = rt_acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
+    if (ang >= PI_D / 2.0) ang = PI_D - ang;
+    const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
+    const Col lc = intensify<FC>(intensify<FC>(Col{lt->col[0], lt->col[1], lt->col[2]}, inten), t);
+    L = cadd<FC>(L, cmul<FC>(c, lc));
+  }
+  if (!have_shading) {
+    shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
+    L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));
+  }
+  bool inside = false;                                                  // :230-235
+  if (depth < max_depth && (refl != 0.0 || (REFR && transp != 0.0))) {
+    const V3 nd = scale(rd, -1.0);
+    inside = inside_test(dot(nd, nrm) / (len(nd) * len(nrm)));
+  }
+  const V3 n2 = inside ? scale(nrm, -1.0) : nrm;
+  const double r1 = inside ? 1.45 : 1.0, r2 = inside ? 1.0 : 1.45;
+  bool tir = false;
+  V3 tdir = {0.0, 0.0, 0.0};
+  const bool do_refr = REFR && depth < max_depth && transp != 0.0;     // :242
+  if (do_refr) tdir = refract_dir(rd, n2, r1 / r2, &tir);
+  const double rp = tir ? refl + (1.0 - refl) * transp : refl;         // :261-265
+  const bool do_refl = depth < max_depth && rp != 0.0 && (!inside || tir);   // :267
+  *Lo = L;
+  *wt = transp;
+  *wr = rp;
+  *ch_t = do_refr && !tir;
+  *ch_r = do_refl;
+  *po = p;
+  *dt = tdir;
+  if (do_refl) *dr = reflect_dir(rd, n2);
+}
+
+#ifndef RT_WAVES_PER_EU_WF
+#define RT_WAVES_PER_EU_WF 5
+#endif
+template <bool REFR, bool FC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_WF))) void wf_trace_kernel(
+    RtDevScene S, WfArena A, int d, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth) {
+  const int lane = threadIdx.x & 63;
+  const DS D = make_ds(S);
+  const WfLevel lv = wf_level(A, d);
+  const WfLevel nx = wf_level(A, d < max_depth ? d + 1 : d);   // no ray spawns at depth max_depth
+  const uint32_t n = d == 0 ? A.slots : min(A.count[d], A.cap);
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (uint32_t base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
+    const uint32_t i = base + (uint32_t)lane;
+    bool live = i < n;
+    V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+    int32_t pix = (int32_t)i;
+    if (d == 0) {
+      int x, r, y;
+      live = live && wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y);
+      if (live) camera_ray(S.cam, (double)x, (double)y, &ro, &rd);          // get_pixel(x as f64, y as f64)
+    } else if (live) {
+      ro = {lv.ox[i], lv.oy[i], lv.oz[i]};
+      rd = {lv.dx[i], lv.dy[i], lv.dz[i]};
+      pix = lv.pix[i];
+    }
+    Col L = {0.0, 0.0, 0.0};
+    double wt = 0.0, wr = 0.0;
+    bool ch_t = false, ch_r = false;
+    V3 p = {0.0, 0.0, 0.0}, dt = {0.0, 0.0, 0.0}, dr = {0.0, 0.0, 0.0};
+    if (live) wf_ray<REFR, FC>(D, ro, rd, d, max_depth, &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr);
+    int32_t ct = -1, cr = -1;
+    const uint64_t bt = __ballot(ch_t), br = __ballot(ch_r);
+    const uint32_t nt = (uint32_t)__popcll(bt), nr = (uint32_t)__popcll(br);
+    if (nt + nr) {
+      uint32_t b0 = 0;
+      if (lane == 0) b0 = atomicAdd(&A.count[d + 1], nt + nr);
+      b0 = (uint32_t)__shfl((int)b0, 0);
+      const uint32_t st = b0 + (uint32_t)__popcll(bt & below), sr = b0 + nt + (uint32_t)__popcll(br & below);
+      bool ovf = false;
+      if (ch_t) {
+        if (st < A.cap) {
+          nx.ox[st] = p.x; nx.oy[st] = p.y; nx.oz[st] = p.z; nx.dx[st] = dt.x; nx.dy[st] = dt.y; nx.dz[st] = dt.z;
+          nx.pix[st] = pix;
+          ct = (int32_t)st;
+        } else ovf = true;
+      }
+      if (ch_r) {
+        if (sr < A.cap) {
+          nx.ox[sr] = p.x; nx.oy[sr] = p.y; nx.oz[sr] = p.z; nx.dx[sr] = dr.x; nx.dy[sr] = dr.y; nx.dz[sr] = dr.z;
+          nx.pix[sr] = pix;
+          cr = (int32_t)sr;
+        } else ovf = true;
+      }
+      if (ovf) {                                                // this pixel is re-rendered by wf_fixup_kernel
+        A.ovf[pix] = 1;
+        A.count[RT_MAX_DEPTH_CAP + 2] = 1;
+      }
+    }
+    if (live) {
+      lv.Lr[i] = L.r; lv.Lg[i] = L.g; lv.Lb[i] = L.b; lv.wt[i] = wt; lv.wr[i] = wr;
+      lv.ct[i] = ct; lv.cr[i] = cr;
+    }
+  }
+}
+
+template <bool F64, bool FC>
+__global__ __launch_bounds__(256) void wf_fold_kernel(RtDevScene S, WfArena A, int d, int y_first, int band_rows,
+                                                      int band_pitch, int n_rows, uint8_t* __restrict__ out,
+                                                      size_t stride, int rgb) {
+  const WfLevel lv = wf_level(A, d);
+  const WfLevel ch = wf_level(A, d + 1);
+  const uint32_t n = d == 0 ? A.slots : min(A.count[d], A.cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int x = 0, r = 0, y = 0;
+    if (d == 0 && (!wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y) || A.ovf[i])) continue;
+    const Col L = {lv.Lr[i], lv.Lg[i], lv.Lb[i]};
+    const int32_t ct = lv.ct[i], cr = lv.cr[i];
+    Col C = L;
+    if (ct >= 0) {                                             // refraction, then a pending reflection
+      const double t = lv.wt[i];
+      C = cadd<FC>(intensify<FC>(L, 1.0 - t), intensify<FC>(Col{ch.Lr[ct], ch.Lg[ct], ch.Lb[ct]}, t));
+    }
+    if (cr >= 0) {
+      const double w = lv.wr[i];
+      C = cadd<FC>(intensify<FC>(C, 1.0 - w), intensify<FC>(Col{ch.Lr[cr], ch.Lg[cr], ch.Lb[cr]}, w));
+    }
+    if (d > 0) {
+      lv.Lr[i] = C.r; lv.Lg[i] = C.g; lv.Lb[i] = C.b;
+      continue;
+    }
+    uint8_t* row = out + (size_t)r * stride;
+    if constexpr (F64) {
+      double* o = (double*)row + (size_t)x * 4;
+      o[0] = C.r; o[1] = C.g; o[2] = C.b; o[3] = 1.0;
+    } else if (rgb) {
+      uint8_t* o = row + (size_t)x * 3;
+      o[0] = (uint8_t)to_u8(C.r); o[1] = (uint8_t)to_u8(C.g); o[2] = (uint8_t)to_u8(C.b);
+    } else {
+      ((uint32_t*)row)[x] = to_u8(C.r) | (to_u8(C.g) << 8) | (to_u8(C.b) << 16) | (255u << 24);
+    }
+  }
+}
+
+// Pixels whose tree overflowed a level: the per-lane megakernel trace (same bits).  Returns at once
+// when no level overflowed (one uniform load).
+template <bool REFR, bool F64, bool FC>
+__global__ __launch_bounds__(64) void wf_fixup_kernel(RtDevScene S, WfArena A, int y_first, int band_rows,
+                                                      int band_pitch, int n_rows, int max_depth,
+                                                      uint8_t* __restrict__ out, size_t stride, int rgb) {
+  if (A.count[RT_MAX_DEPTH_CAP + 2] == 0) return;
+  for (uint32_t i = blockIdx.x * 64 + threadIdx.x; i < A.slots; i += gridDim.x * 64) {
+    int x, r, y;
+    if (!A.ovf[i] || !wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y)) continue;
+    V3 ro, rd;
+    camera_ray(S.cam, (double)x, (double)y, &ro, &rd);
+    const Col C = trace<REFR, NoRec, 0, FC>(make_ds(S), ro, rd, max_depth);
+    uint8_t* row = out + (size_t)r * stride;
+    if constexpr (F64) {
+      double* o = (double*)row + (size_t)x * 4;
+      o[0] = C.r; o[1] = C.g; o[2] = C.b; o[3] = 1.0;
+    } else if (rgb) {
+      uint8_t* o = row + (size_t)x * 3;
+      o[0] = (uint8_t)to_u8(C.r); o[1] = (uint8_t)to_u8(C.g); o[2] = (uint8_t)to_u8(C.b);
+    } else {
+      ((uint32_t*)row)[x] = to_u8(C.r) | (to_u8(C.g) << 8) | (to_u8(C.b) << 16) | (255u << 24);
+    }
+  }
+}
+
 template <bool REFR>
 __global__ void record_ray_kernel(RtDevScene S, double x, double y, int max_depth, RtRayRecord* rec, int* order,
                                   int cap, int* counts) {
@@ -1688,12 +1940,15 @@ struct rt_ctx {
   bool timing = true;                   // rt_ctx_set_option(RT_OPT_TIMING): launch events recorded
   bool tile_order = true;               // rt_ctx_set_option(RT_OPT_TILE_ORDER): cost-ordered dispatch
   bool fast_clamp = true;               // rt_ctx_set_option(RT_OPT_FAST_CLAMP): min/max clamps where exact
+  int wf_cap_pct = 200;                 // rt_ctx_set_option(RT_OPT_WAVEFRONT_CAP): rays per level, % of pixel slots
   int n_cu = 256;                       // compute units of the device (wave slots = n_cu x 4 SIMDs x waves/SIMD)
   bool uploaded = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  void* wf = nullptr;                   // wavefront arena (levels, counters, overflow flags), grow-only
+  size_t wf_bytes = 0;
   // Cost-ordered tile dispatch.  A frame's time is set by its slowest tiles (long reflection
   // chains), so they are dispatched first: the first launch of a geometry records every tile's
   // wave time, and later launches of the same geometry read the tiles in descending cost order.
@@ -1894,6 +2149,57 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   return RT_OK;
 }
 
+// The wavefront path (wf_*_kernel): levels 0..max_depth traced in order, then folded deepest first,
+// then the overflow fix-up; all on the launch stream, no host synchronisation.
+static int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int a3, int max_depth, uint8_t* target,
+                            size_t tstride, bool f64, int rgbi, size_t n_tiles) {
+  const size_t slots = n_tiles * 64, cap = std::max<size_t>(64, (slots * (size_t)c->wf_cap_pct / 100 + 63) & ~(size_t)63);
+  if (cap > 0x7fffffffull) return fail(RT_ERR_UNSUPPORTED, "wavefront launch of %zu pixel slots too large", slots);
+  const size_t levels = slots * RT_WF_BYTES0 + (size_t)max_depth * cap * RT_WF_BYTES;
+  const size_t o_cnt = (levels + 255) & ~(size_t)255, o_ovf = o_cnt + 256, bytes = o_ovf + slots + 256;
+  if (c->wf_bytes < bytes) {
+    if (c->wf) (void)hipFree(c->wf);          // waits for launches that may still use it
+    c->wf = nullptr;
+    c->wf_bytes = 0;
+    RT_HIP(hipMalloc(&c->wf, bytes));
+    c->wf_bytes = bytes;
+  }
+  WfArena A;
+  A.base = (uint8_t*)c->wf;
+  A.count = (uint32_t*)(A.base + o_cnt);
+  A.ovf = A.base + o_ovf;
+  A.slots = (uint32_t)slots;
+  A.cap = (uint32_t)cap;
+  RT_HIP(hipMemsetAsync(A.count, 0, 256, st));
+  RT_HIP(hipMemsetAsync(A.ovf, 0, slots, st));
+  const bool refr = c->dev.any_transparent != 0, fc = c->dev.colour_fast != 0 && c->fast_clamp;
+  const unsigned resident = (unsigned)c->n_cu * 4u * RT_WAVES_PER_EU_WF;
+  const unsigned g0 = (unsigned)std::min<size_t>(n_tiles, resident), g1 = (unsigned)std::min<size_t>(cap / 64, resident);
+  for (int d = 0; d <= max_depth; ++d) {
+    const dim3 g(d == 0 ? g0 : g1);
+    if (refr && fc) hipLaunchKernelGGL((wf_trace_kernel<true, true>), g, dim3(64), 0, st, c->dev, A, d, a0, a1, a2, a3, max_depth);
+    else if (refr) hipLaunchKernelGGL((wf_trace_kernel<true, false>), g, dim3(64), 0, st, c->dev, A, d, a0, a1, a2, a3, max_depth);
+    else if (fc) hipLaunchKernelGGL((wf_trace_kernel<false, true>), g, dim3(64), 0, st, c->dev, A, d, a0, a1, a2, a3, max_depth);
+    else hipLaunchKernelGGL((wf_trace_kernel<false, false>), g, dim3(64), 0, st, c->dev, A, d, a0, a1, a2, a3, max_depth);
+  }
+  const dim3 gf((unsigned)c->n_cu * 8u), bf(256);
+  for (int d = max_depth; d >= 0; --d) {
+    if (f64 && fc) hipLaunchKernelGGL((wf_fold_kernel<true, true>), gf, bf, 0, st, c->dev, A, d, a0, a1, a2, a3, target, tstride, rgbi);
+    else if (f64) hipLaunchKernelGGL((wf_fold_kernel<true, false>), gf, bf, 0, st, c->dev, A, d, a0, a1, a2, a3, target, tstride, rgbi);
+    else if (fc) hipLaunchKernelGGL((wf_fold_kernel<false, true>), gf, bf, 0, st, c->dev, A, d, a0, a1, a2, a3, target, tstride, rgbi);
+    else hipLaunchKernelGGL((wf_fold_kernel<false, false>), gf, bf, 0, st, c->dev, A, d, a0, a1, a2, a3, target, tstride, rgbi);
+  }
+  const dim3 gx((unsigned)c->n_cu * 4u);
+#define RT_WF_FIX(R, F, FCv) hipLaunchKernelGGL((wf_fixup_kernel<R, F, FCv>), gx, dim3(64), 0, st, c->dev, A, a0, a1, a2, a3, max_depth, target, tstride, rgbi)
+  if (refr && f64) { if (fc) RT_WF_FIX(true, true, true); else RT_WF_FIX(true, true, false); }
+  else if (refr) { if (fc) RT_WF_FIX(true, false, true); else RT_WF_FIX(true, false, false); }
+  else if (f64) { if (fc) RT_WF_FIX(false, true, true); else RT_WF_FIX(false, true, false); }
+  else { if (fc) RT_WF_FIX(false, false, true); else RT_WF_FIX(false, false, false); }
+#undef RT_WF_FIX
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}
+
 static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_t band_pitch, uint32_t n_bands,
                         int32_t max_depth, void* out, size_t stride, void* stream, bool f64, bool rgb = false) {
   if (!c || !out) return fail(RT_ERR_INVALID, "null argument");
@@ -1926,6 +2232,18 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   const int a0 = (int)y_first, a1 = (int)band_rows, a2 = (int)band_pitch, a3 = (int)n_rows;
   // Tile order: reuse the measured order for this exact geometry, else calibrate on this launch.
   const size_t n_tiles = (size_t)tiles_x * (size_t)tiles_y;
+  if (c->kernel_opt == RT_KERNEL_WAVEFRONT) {
+    if (c->timing) RT_HIP(hipEventRecord(c->ev0, st));
+    int rc = launch_wavefront(c, st, a0, a1, a2, a3, max_depth, target, tstride, f64, rgbi, n_tiles);
+    if (rc) return rc;
+    if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
+    c->timed = c->timing;
+    if (!dev_out) {
+      RT_HIP(hipMemcpy2DAsync(out, stride, target, tstride, row_bytes, n_rows, hipMemcpyDeviceToHost, st));
+      RT_HIP(hipStreamSynchronize(st));
+    }
+    return RT_OK;
+  }
   const int32_t key[7] = {a0, a1, a2, a3, max_depth, f64 ? 1 : 0, c->dev.width};
   const bool refr = c->dev.any_transparent != 0;
   // Kernel choice for scenes without a transparent object (RT_DEFERRED_MAX_TILES): the per-lane
@@ -1937,8 +2255,12 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
 #else
   const bool chain = refr && c->dev.ray_chains != 0;
 #endif
-  // the deferred kernel takes scenes whose rays form chains (reflection-only, or refraction chains)
+  // the deferred kernel takes scenes whose rays form chains (reflection-only, or refraction chains);
+  // the library's own choice (AUTO) takes it for reflection-only scenes only: on refraction chains it
+  // measured 3.2x slower than the chain megakernel (spinning_globes 1080p lone frame 0.80 vs 0.25 ms,
+  // profiles/r03b_chain_ab.txt), so there it runs only when RT_KERNEL_DEFERRED asks for it
   const bool eligible = (!refr || chain) && c->dev.n_lights <= RT_SH_TRCAP && n_tiles <= (size_t)RT_SPLIT_TILE_MASK + 1;
+  const bool auto_ok = eligible && !refr;
   // -1 auto, 0 megakernel, 1 deferred (the context's RT_OPT_KERNEL)
   const int dmode = c->kernel_opt == RT_KERNEL_MEGA ? 0 : c->kernel_opt == RT_KERNEL_DEFERRED ? 1 : -1;
   rt_ctx::OrderSlot* slot = nullptr;
@@ -1969,6 +2291,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   bool deferred;
   if (!eligible || dmode == 0) deferred = false;
   else if (dmode == 1) deferred = true;
+  else if (!auto_ok) deferred = false;
   else if (order) deferred = slot->deferred;
   else if (calibrate) deferred = false;                       // calibrate on the megakernel
   else deferred = n_tiles < RT_ORDER_MIN_TILES || (!c->tile_order && n_tiles < RT_DEFERRED_MAX_TILES);
@@ -2020,7 +2343,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     bool tail_bound = false;
     // wave slots of the calibrated (mega)kernel on this device
     const double slots = (double)c->n_cu * 4.0 * (double)(!refr ? RT_WAVES_PER_EU_NOREFR : c->dev.ray_chains ? RT_WAVES_PER_EU_CHAIN : RT_WAVES_PER_EU);
-    if (eligible && dmode == -1 && n_tiles < RT_DEFERRED_MAX_TILES) {
+    if (auto_ok && dmode == -1 && n_tiles < RT_DEFERRED_MAX_TILES) {
       uint64_t sum = 0, mx = 0;
       for (uint32_t v : h_cost) { sum += v; mx = v > mx ? v : mx; }
       tail_bound = (double)mx > (double)sum / slots;
@@ -2387,6 +2710,11 @@ int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
     c->timed = false;                  // no launch recorded under the new setting yet
     return RT_OK;
   }
+  if (option == RT_OPT_WAVEFRONT_CAP) {
+    if (value < 1 || value > 400) return fail(RT_ERR_INVALID, "RT_OPT_WAVEFRONT_CAP %d not in [1, 400]", value);
+    c->wf_cap_pct = value;
+    return RT_OK;
+  }
   if (option == RT_OPT_TILE_ORDER || option == RT_OPT_FAST_CLAMP) {
     if (value != 0 && value != 1) return fail(RT_ERR_INVALID, "option %d value %d", option, value);
     if (option == RT_OPT_FAST_CLAMP) {
@@ -2399,7 +2727,7 @@ int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
     return RT_OK;
   }
   if (option != RT_OPT_KERNEL) return fail(RT_ERR_INVALID, "unknown option %d", option);
-  if (value != RT_KERNEL_AUTO && value != RT_KERNEL_MEGA && value != RT_KERNEL_DEFERRED)
+  if (value != RT_KERNEL_AUTO && value != RT_KERNEL_MEGA && value != RT_KERNEL_DEFERRED && value != RT_KERNEL_WAVEFRONT)
     return fail(RT_ERR_INVALID, "RT_OPT_KERNEL value %d", value);
   if (value != c->kernel_opt) {
     // tile orders were built for one kernel (split entries only for the deferred one): rebuild
@@ -2446,6 +2774,7 @@ void rt_ctx_free(rt_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   if (c->d_blob) (void)hipFree(c->d_blob);
   if (c->scratch) (void)hipFree(c->scratch);
+  if (c->wf) (void)hipFree(c->wf);
   drop_orders(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);

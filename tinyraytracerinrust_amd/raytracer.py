@@ -276,8 +276,10 @@ class Renderer:
         return out
 
     def set_kernel(self, kernel: str = "auto") -> None:
-        """rt_ctx_set_option(RT_OPT_KERNEL): "auto", "mega" or "deferred" (same pixels; see rt_abi.h)."""
-        v = {"auto": _lib.RT_KERNEL_AUTO, "mega": _lib.RT_KERNEL_MEGA, "deferred": _lib.RT_KERNEL_DEFERRED}[kernel]
+        """rt_ctx_set_option(RT_OPT_KERNEL): "auto", "mega", "deferred" or "wavefront" (same pixels;
+        see rt_abi.h)."""
+        v = {"auto": _lib.RT_KERNEL_AUTO, "mega": _lib.RT_KERNEL_MEGA, "deferred": _lib.RT_KERNEL_DEFERRED,
+             "wavefront": _lib.RT_KERNEL_WAVEFRONT}[kernel]
         check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_KERNEL, v))
 
     def set_timing(self, on: bool) -> None:
@@ -294,6 +296,11 @@ class Renderer:
         """rt_ctx_set_option(RT_OPT_FAST_CLAMP): min/max colour clamps where the host proved them exact
         (default) or the reference's compare/select clamps everywhere (same pixels)."""
         check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_FAST_CLAMP, 1 if on else 0))
+
+    def set_wavefront_cap(self, percent: int) -> None:
+        """rt_ctx_set_option(RT_OPT_WAVEFRONT_CAP): rays per recursion level of the wavefront path, in
+        percent of the launch's pixel slots (pixels whose tree overflows are re-rendered, same bits)."""
+        check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_WAVEFRONT_CAP, int(percent)))
 
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()

@@ -19,7 +19,7 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--frames", type=int, default=60)
     ap.add_argument("--depth", type=int, default=10)
-    ap.add_argument("--kernel", default="bench", choices=["bench", "auto", "mega", "deferred"])
+    ap.add_argument("--kernel", default="bench", choices=["bench", "auto", "mega", "deferred", "wavefront"])
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--ks", default="1,2,3,4")
     ap.add_argument("--reps", type=int, default=1, help="repeat each (N, K) with a fresh context (new calibration)")
@@ -61,7 +61,7 @@ def main():
                     cx, sc = cx0
                     streams = fixed if a.fixed_streams else new_streams()
                     mode = ("auto" if k == 1 else "mega") if a.kernel == "bench" else a.kernel
-                    assert L.rt_ctx_set_option(cx, 0, {"auto": 0, "mega": 1, "deferred": 2}[mode]) == 0   # RT_OPT_KERNEL
+                    assert L.rt_ctx_set_option(cx, 0, {"auto": 0, "mega": 1, "deferred": 2, "wavefront": 3}[mode]) == 0   # RT_OPT_KERNEL
 
                     def issue(i):
                         s = streams[i % k]
