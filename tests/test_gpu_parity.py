@@ -332,7 +332,8 @@ def test_rgb8_row_bands_assemble_like_ranks(T, world, layout, band):
 def test_assemble_rgb8_kernel_random(T):
     import torch
     from tinyraytracerinrust_amd import distributed as D
-    for W, H, world, band in [(3840, 2160, 8, 8), (33, 61, 3, 5)]:
+    # 3840 / 1924: the 4-pixel (12-byte load, 16-byte store) path; 33 / 1922: one pixel per thread
+    for W, H, world, band in [(3840, 2160, 8, 8), (33, 61, 3, 5), (1924, 100, 8, 8), (1922, 64, 2, 8)]:
         slot_rows = D.rows_per_rank(H, world, "cyclic", band)
         g = torch.randint(0, 256, (world * slot_rows, W, 3), dtype=torch.uint8, device="cuda")
         want = D.assemble_reference(g, H, world, "cyclic", band).cpu()

@@ -1355,9 +1355,13 @@ render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_p
 // ray of recursion depth d of the launch, densely, one lane per ray.  Per level:
 //   wf_trace_kernel  nearest hit, shadow rays, shading, the inside / refraction / TIR / reflection
 //                    decisions of trace() (the same operations in the same order); the rays a hit
-//                    spawns are appended to level d + 1 (one ballot + one atomic per wave: a wave's
-//                    refraction children, then its reflection children, keep their lanes' order), the
-//                    hit record (L, the two weights, the children's slots) stays at its slot;
+//                    spawns are appended to level d + 1 (one ballot + one atomic per wave), each with a
+//                    coherence key (direction octant, Morton code of its origin); the hit record (L,
+//                    the two weights, the children's slots) stays at the ray's slot;
+//   sort             level d + 1's slots by key (rocPRIM radix sort of (key, slot) pairs): a wave of
+//                    the next pass then traces rays that start close together in similar directions,
+//                    so the wave-coherent traversal walks fewer objects (the megakernel's waves walk the
+//                    union of what their lanes' scattered secondary rays need);
 //   wf_fold_kernel   after every level is traced, from the deepest level up: a ray's colour from its
 //                    hit record and its children's colours (already folded into their L slots):
 //                      refraction child: comb = in_range(L.intensify(1 - t) + C_t.intensify(t)),
@@ -1365,22 +1369,28 @@ render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_p
 //                    exactly the post-order of raytracer.rs:256-279 (trace()'s frame fold).  Level 0's
 //                    fold writes the pixels.
 // Lanes whose pixel's tree ended early no longer idle in its wave (the megakernel's per-lane tree
-// walk keeps a wave alive for its deepest tree): every pass starts with every lane on a live ray.
-// Levels >= 1 hold up to 2 x the launch's pixel slots; a ray that finds its level full marks its
-// pixel, and wf_fixup_kernel re-renders marked pixels with trace() (same bits, rarely taken).
+// walk keeps a wave alive for its deepest tree): every pass starts with every lane on a live ray, and
+// every pass is one workgroup per 64 rays, so the hardware dispatcher balances uneven rays.  The
+// host reads each level's count before launching it (one synchronisation per level: this path is
+// for heavy, incoherent launches).  Levels >= 1 hold RT_OPT_WAVEFRONT_CAP % of the pixel slots; a
+// ray that finds its level full marks its pixel, and wf_fixup_kernel re-renders marked pixels with
+// trace() (same bits).
 struct WfArena {
   uint8_t* base;          // level tables (wf_level)
   uint32_t* count;        // count[d]: rays appended to level d (d >= 1); count[RT_MAX_DEPTH_CAP + 2]: any overflow
   uint8_t* ovf;           // per pixel slot: its tree overflowed a level
+  const uint32_t* perm;   // the level being traced: slot of its i-th ray in key order (null: slot order)
   uint32_t slots, cap;    // level 0 = the pixel slots (8x8 tiles x 64), levels >= 1: cap rays each
+  double klo[3], kscale[3];   // origin -> 9-bit cell per axis for the coherence keys
 };
 struct WfLevel {
   double *ox, *oy, *oz, *dx, *dy, *dz;   // levels >= 1: the ray
   double *Lr, *Lg, *Lb, *wt, *wr;        // hit record: L (then the folded colour), refraction / reflection weights
   int32_t *pix, *ct, *cr;                // pixel slot (levels >= 1), children's slots in level d + 1 (-1: none)
+  uint32_t *key, *val;                   // levels >= 1: coherence key and slot (the sort's input pairs)
 };
-constexpr size_t RT_WF_BYTES0 = 5 * 8 + 2 * 4, RT_WF_BYTES = 11 * 8 + 3 * 4;
-__device__ __forceinline__ WfLevel wf_level(const WfArena& A, int d) {
+constexpr size_t RT_WF_BYTES0 = 5 * 8 + 2 * 4, RT_WF_BYTES = 11 * 8 + 5 * 4;
+__host__ __device__ __forceinline__ WfLevel wf_level(const WfArena& A, int d) {
   WfLevel v;
   const size_t len = d == 0 ? A.slots : A.cap;
   double* f = (double*)(A.base + (d == 0 ? 0 : (size_t)A.slots * RT_WF_BYTES0 + (size_t)(d - 1) * A.cap * RT_WF_BYTES));
@@ -1389,11 +1399,13 @@ __device__ __forceinline__ WfLevel wf_level(const WfArena& A, int d) {
     v.Lr = f; v.Lg = f + len; v.Lb = f + 2 * len; v.wt = f + 3 * len; v.wr = f + 4 * len;
     int32_t* q = (int32_t*)(f + 5 * len);
     v.pix = nullptr; v.ct = q; v.cr = q + len;
+    v.key = v.val = nullptr;
   } else {
     v.ox = f; v.oy = f + len; v.oz = f + 2 * len; v.dx = f + 3 * len; v.dy = f + 4 * len; v.dz = f + 5 * len;
     v.Lr = f + 6 * len; v.Lg = f + 7 * len; v.Lb = f + 8 * len; v.wt = f + 9 * len; v.wr = f + 10 * len;
     int32_t* q = (int32_t*)(f + 11 * len);
     v.pix = q; v.ct = q + len; v.cr = q + 2 * len;
+    v.key = (uint32_t*)(q + 3 * len); v.val = (uint32_t*)(q + 4 * len);
   }
   return v;
 }
@@ -1406,6 +1418,26 @@ __device__ __forceinline__ bool wf_pixel(const RtDevScene& S, uint32_t slot, int
   if (*x >= S.width || *r >= n_rows) return false;
   *y = y_first + (*r / band_rows) * band_pitch + *r % band_rows;
   return *y < S.height;
+}
+// coherence key of a ray: direction octant (3 bits) above the 27-bit Morton code of its origin's
+// cell (9 bits per axis over the scene's bounded extent, clamped).  Only the processing order
+// depends on it, never a value.
+__device__ __forceinline__ uint32_t wf_spread9(uint32_t v) {            // 9 bits -> every third bit
+  v &= 511u;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+__device__ __forceinline__ uint32_t wf_key(const WfArena& A, V3 o, V3 d) {
+  auto cell = [](double x, double lo, double sc) -> uint32_t {
+    const double c = (x - lo) * sc;
+    return c > 0.0 ? (c < 511.0 ? (uint32_t)c : 511u) : 0u;           // NaN -> 0
+  };
+  const uint32_t oct = (d.x < 0.0 ? 1u : 0u) | (d.y < 0.0 ? 2u : 0u) | (d.z < 0.0 ? 4u : 0u);
+  return (oct << 27) | wf_spread9(cell(o.x, A.klo[0], A.kscale[0])) | (wf_spread9(cell(o.y, A.klo[1], A.kscale[1])) << 1) |
+         (wf_spread9(cell(o.z, A.klo[2], A.kscale[2])) << 2);
 }
 
 // One ray of trace()'s loop body: nearest hit, the light loop (shadow rays first, then the shading
@@ -1475,76 +1507,75 @@ __device__ __forceinline__ void wf_ray(const DS& S, V3 ro, V3 rd, int depth, int
 #ifndef RT_WAVES_PER_EU_WF
 #define RT_WAVES_PER_EU_WF 5
 #endif
+// One workgroup (wave) per 64 rays of level d (n of them): level 0 = the pixel slots in tile order,
+// levels >= 1 in key order (A.perm).
 template <bool REFR, bool FC>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_WF))) void wf_trace_kernel(
-    RtDevScene S, WfArena A, int d, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth) {
+    RtDevScene S, WfArena A, int d, uint32_t n, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth) {
   const int lane = threadIdx.x & 63;
-  const DS D = make_ds(S);
+  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+  bool live = i < n;
   const WfLevel lv = wf_level(A, d);
-  const WfLevel nx = wf_level(A, d < max_depth ? d + 1 : d);   // no ray spawns at depth max_depth
-  const uint32_t n = d == 0 ? A.slots : min(A.count[d], A.cap);
-  const uint64_t below = (1ull << lane) - 1ull;
-  for (uint32_t base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
-    const uint32_t i = base + (uint32_t)lane;
-    bool live = i < n;
-    V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
-    int32_t pix = (int32_t)i;
-    if (d == 0) {
-      int x, r, y;
-      live = live && wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y);
-      if (live) camera_ray(S.cam, (double)x, (double)y, &ro, &rd);          // get_pixel(x as f64, y as f64)
-    } else if (live) {
-      ro = {lv.ox[i], lv.oy[i], lv.oz[i]};
-      rd = {lv.dx[i], lv.dy[i], lv.dz[i]};
-      pix = lv.pix[i];
+  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+  uint32_t j = i;                                            // the ray's slot in its level
+  int32_t pix = (int32_t)i;
+  if (d == 0) {
+    int x, r, y;
+    live = live && wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y);
+    if (live) camera_ray(S.cam, (double)x, (double)y, &ro, &rd);          // get_pixel(x as f64, y as f64)
+  } else if (live) {
+    j = A.perm ? A.perm[i] : i;
+    ro = {lv.ox[j], lv.oy[j], lv.oz[j]};
+    rd = {lv.dx[j], lv.dy[j], lv.dz[j]};
+    pix = lv.pix[j];
+  }
+  Col L = {0.0, 0.0, 0.0};
+  double wt = 0.0, wr = 0.0;
+  bool ch_t = false, ch_r = false;
+  V3 p = {0.0, 0.0, 0.0}, dt = {0.0, 0.0, 0.0}, dr = {0.0, 0.0, 0.0};
+  if (live) wf_ray<REFR, FC>(make_ds(S), ro, rd, d, max_depth, &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr);
+  int32_t ct = -1, cr = -1;
+  const uint64_t bt = __ballot(ch_t), br = __ballot(ch_r);
+  const uint32_t nt = (uint32_t)__popcll(bt), nr = (uint32_t)__popcll(br);
+  if (nt + nr) {                                             // wave-uniform: d < max_depth here
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t b0 = 0;
+    if (lane == 0) b0 = atomicAdd(&A.count[d + 1], nt + nr);
+    b0 = (uint32_t)__shfl((int)b0, 0);
+    const WfLevel nx = wf_level(A, d + 1);
+    const uint32_t st = b0 + (uint32_t)__popcll(bt & below), sr = b0 + nt + (uint32_t)__popcll(br & below);
+    bool ovf = false;
+    if (ch_t) {
+      if (st < A.cap) {
+        nx.ox[st] = p.x; nx.oy[st] = p.y; nx.oz[st] = p.z; nx.dx[st] = dt.x; nx.dy[st] = dt.y; nx.dz[st] = dt.z;
+        nx.pix[st] = pix; nx.key[st] = wf_key(A, p, dt); nx.val[st] = st;
+        ct = (int32_t)st;
+      } else ovf = true;
     }
-    Col L = {0.0, 0.0, 0.0};
-    double wt = 0.0, wr = 0.0;
-    bool ch_t = false, ch_r = false;
-    V3 p = {0.0, 0.0, 0.0}, dt = {0.0, 0.0, 0.0}, dr = {0.0, 0.0, 0.0};
-    if (live) wf_ray<REFR, FC>(D, ro, rd, d, max_depth, &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr);
-    int32_t ct = -1, cr = -1;
-    const uint64_t bt = __ballot(ch_t), br = __ballot(ch_r);
-    const uint32_t nt = (uint32_t)__popcll(bt), nr = (uint32_t)__popcll(br);
-    if (nt + nr) {
-      uint32_t b0 = 0;
-      if (lane == 0) b0 = atomicAdd(&A.count[d + 1], nt + nr);
-      b0 = (uint32_t)__shfl((int)b0, 0);
-      const uint32_t st = b0 + (uint32_t)__popcll(bt & below), sr = b0 + nt + (uint32_t)__popcll(br & below);
-      bool ovf = false;
-      if (ch_t) {
-        if (st < A.cap) {
-          nx.ox[st] = p.x; nx.oy[st] = p.y; nx.oz[st] = p.z; nx.dx[st] = dt.x; nx.dy[st] = dt.y; nx.dz[st] = dt.z;
-          nx.pix[st] = pix;
-          ct = (int32_t)st;
-        } else ovf = true;
-      }
-      if (ch_r) {
-        if (sr < A.cap) {
-          nx.ox[sr] = p.x; nx.oy[sr] = p.y; nx.oz[sr] = p.z; nx.dx[sr] = dr.x; nx.dy[sr] = dr.y; nx.dz[sr] = dr.z;
-          nx.pix[sr] = pix;
-          cr = (int32_t)sr;
-        } else ovf = true;
-      }
-      if (ovf) {                                                // this pixel is re-rendered by wf_fixup_kernel
-        A.ovf[pix] = 1;
-        A.count[RT_MAX_DEPTH_CAP + 2] = 1;
-      }
+    if (ch_r) {
+      if (sr < A.cap) {
+        nx.ox[sr] = p.x; nx.oy[sr] = p.y; nx.oz[sr] = p.z; nx.dx[sr] = dr.x; nx.dy[sr] = dr.y; nx.dz[sr] = dr.z;
+        nx.pix[sr] = pix; nx.key[sr] = wf_key(A, p, dr); nx.val[sr] = sr;
+        cr = (int32_t)sr;
+      } else ovf = true;
     }
-    if (live) {
-      lv.Lr[i] = L.r; lv.Lg[i] = L.g; lv.Lb[i] = L.b; lv.wt[i] = wt; lv.wr[i] = wr;
-      lv.ct[i] = ct; lv.cr[i] = cr;
+    if (ovf) {                                                // this pixel is re-rendered by wf_fixup_kernel
+      A.ovf[pix] = 1;
+      A.count[RT_MAX_DEPTH_CAP + 2] = 1;
     }
+  }
+  if (live) {
+    lv.Lr[j] = L.r; lv.Lg[j] = L.g; lv.Lb[j] = L.b; lv.wt[j] = wt; lv.wr[j] = wr;
+    lv.ct[j] = ct; lv.cr[j] = cr;
   }
 }
 
 template <bool F64, bool FC>
-__global__ __launch_bounds__(256) void wf_fold_kernel(RtDevScene S, WfArena A, int d, int y_first, int band_rows,
-                                                      int band_pitch, int n_rows, uint8_t* __restrict__ out,
-                                                      size_t stride, int rgb) {
+__global__ __launch_bounds__(256) void wf_fold_kernel(RtDevScene S, WfArena A, int d, uint32_t n, int y_first,
+                                                      int band_rows, int band_pitch, int n_rows,
+                                                      uint8_t* __restrict__ out, size_t stride, int rgb) {
   const WfLevel lv = wf_level(A, d);
   const WfLevel ch = wf_level(A, d + 1);
-  const uint32_t n = d == 0 ? A.slots : min(A.count[d], A.cap);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int x = 0, r = 0, y = 0;
     if (d == 0 && (!wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y) || A.ovf[i])) continue;
@@ -1912,14 +1943,29 @@ __global__ __launch_bounds__(256) void assemble_bands_kernel(const uint8_t* __re
 }
 
 // The same placement from packed RGB8 slot rows (3 bytes per pixel, rt_render_row_bands_rgb8) into
-// RGBA8 frame rows with A = 255: the all-gather moves 3/4 of the bytes.  One workgroup per row,
-// one pixel per thread and iteration (3 byte loads, one 4-byte store).
+// RGBA8 frame rows with A = 255: the all-gather moves 3/4 of the bytes.  One workgroup per row.
+// vec: 4 pixels per thread and iteration -- three 4-byte loads (12 bytes = 4 RGB pixels) and one
+// 16-byte store -- when the slot rows are 4-byte and the frame rows 16-byte aligned and the width
+// is a multiple of 4; otherwise one pixel per thread (3 byte loads, one 4-byte store).
 __global__ __launch_bounds__(256) void assemble_bands_rgb_kernel(const uint8_t* __restrict__ g, size_t gstride,
                                                                  int world, int slot_rows, int band, int width,
-                                                                 uint8_t* __restrict__ f, size_t fstride) {
+                                                                 uint8_t* __restrict__ f, size_t fstride, int vec) {
   const int y = blockIdx.x, b = y / band;
   const uint8_t* s = g + ((size_t)(b % world) * slot_rows + (size_t)(b / world) * band + y % band) * gstride;
   uint32_t* d = (uint32_t*)(f + (size_t)y * fstride);
+  if (vec) {
+    const uint32_t* s4 = (const uint32_t*)s;
+    for (int q = threadIdx.x; q < width / 4; q += blockDim.x) {
+      const uint32_t w0 = s4[3 * q], w1 = s4[3 * q + 1], w2 = s4[3 * q + 2];
+      uint4 o;
+      o.x = (w0 & 0xFFFFFFu) | 0xFF000000u;
+      o.y = (w0 >> 24) | ((w1 & 0xFFFFu) << 8) | 0xFF000000u;
+      o.z = (w1 >> 16) | ((w2 & 0xFFu) << 16) | 0xFF000000u;
+      o.w = (w2 >> 8) | 0xFF000000u;
+      ((uint4*)d)[q] = o;
+    }
+    return;
+  }
   for (int x = threadIdx.x; x < width; x += blockDim.x) {
     const uint8_t* p = s + (size_t)x * 3;
     d[x] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | (255u << 24);
@@ -1941,6 +1987,7 @@ struct rt_ctx {
   bool tile_order = true;               // rt_ctx_set_option(RT_OPT_TILE_ORDER): cost-ordered dispatch
   bool fast_clamp = true;               // rt_ctx_set_option(RT_OPT_FAST_CLAMP): min/max clamps where exact
   int wf_cap_pct = 200;                 // rt_ctx_set_option(RT_OPT_WAVEFRONT_CAP): rays per level, % of pixel slots
+  double wf_klo[3] = {-100, -100, -100}, wf_khi[3] = {100, 100, 100};   // coherence-key extent (bounded objects)
   int n_cu = 256;                       // compute units of the device (wave slots = n_cu x 4 SIMDs x waves/SIMD)
   bool uploaded = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -2144,19 +2191,39 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   d.ray_chains = f.ray_chains;
   d.cam = f.cam;
   c->max_depth = f.max_depth;
+  {                                   // the wavefront path's key extent: the hull of the bounded objects
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (const RtObject& o : f.objects)
+      if (o.cull == RT_CULL_BOX)
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], o.blo[k]); hi[k] = std::max(hi[k], o.bhi[k]); }
+    for (int k = 0; k < 3; ++k) {
+      const bool ok = std::isfinite(lo[k]) && std::isfinite(hi[k]) && hi[k] > lo[k];
+      c->wf_klo[k] = ok ? lo[k] : f.cam.center[k] - 100.0;
+      c->wf_khi[k] = ok ? hi[k] : f.cam.center[k] + 100.0;
+    }
+  }
   c->uploaded = true;
   drop_orders(c);                     // tile costs belong to the previous scene
   return RT_OK;
 }
 
-// The wavefront path (wf_*_kernel): levels 0..max_depth traced in order, then folded deepest first,
-// then the overflow fix-up; all on the launch stream, no host synchronisation.
+extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                                       const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit,
+                                       hipStream_t stream);
+
+// The wavefront path (wf_*_kernel): level 0 (the pixel slots), then each level the previous one
+// appended to, sorted by coherence key; then the folds, deepest level first; then the overflow
+// fix-up.  The host reads every level's ray count (one stream synchronisation per level) to launch
+// exactly one wave per 64 rays and to stop at the first empty level.
 static int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int a3, int max_depth, uint8_t* target,
                             size_t tstride, bool f64, int rgbi, size_t n_tiles) {
   const size_t slots = n_tiles * 64, cap = std::max<size_t>(64, (slots * (size_t)c->wf_cap_pct / 100 + 63) & ~(size_t)63);
-  if (cap > 0x7fffffffull) return fail(RT_ERR_UNSUPPORTED, "wavefront launch of %zu pixel slots too large", slots);
+  if (cap > 0x7fffffffull || slots > 0x7fffffffull) return fail(RT_ERR_UNSUPPORTED, "wavefront launch of %zu pixel slots too large", slots);
+  size_t sort_bytes = 0;
+  RT_HIP(rt_wf_sort_pairs(nullptr, &sort_bytes, nullptr, nullptr, nullptr, nullptr, (int)cap, 30, st));
   const size_t levels = slots * RT_WF_BYTES0 + (size_t)max_depth * cap * RT_WF_BYTES;
-  const size_t o_cnt = (levels + 255) & ~(size_t)255, o_ovf = o_cnt + 256, bytes = o_ovf + slots + 256;
+  const size_t o_cnt = (levels + 255) & ~(size_t)255, o_ovf = o_cnt + 256, o_kout = (o_ovf + slots + 255) & ~(size_t)255;
+  const size_t o_perm = o_kout + cap * 4, o_tmp = (o_perm + cap * 4 + 255) & ~(size_t)255, bytes = o_tmp + sort_bytes + 256;
   if (c->wf_bytes < bytes) {
     if (c->wf) (void)hipFree(c->wf);          // waits for launches that may still use it
     c->wf = nullptr;
@@ -2164,30 +2231,59 @@ static int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, i
     RT_HIP(hipMalloc(&c->wf, bytes));
     c->wf_bytes = bytes;
   }
+  uint8_t* base = (uint8_t*)c->wf;
   WfArena A;
-  A.base = (uint8_t*)c->wf;
-  A.count = (uint32_t*)(A.base + o_cnt);
-  A.ovf = A.base + o_ovf;
+  A.base = base;
+  A.count = (uint32_t*)(base + o_cnt);
+  A.ovf = base + o_ovf;
+  A.perm = nullptr;
   A.slots = (uint32_t)slots;
   A.cap = (uint32_t)cap;
+  for (int k = 0; k < 3; ++k) {
+    A.klo[k] = c->wf_klo[k];
+    A.kscale[k] = 512.0 / std::max(1e-9, c->wf_khi[k] - c->wf_klo[k]);
+  }
+  uint32_t* kout = (uint32_t*)(base + o_kout);
+  uint32_t* perm = (uint32_t*)(base + o_perm);
+  void* tmp = base + o_tmp;
   RT_HIP(hipMemsetAsync(A.count, 0, 256, st));
   RT_HIP(hipMemsetAsync(A.ovf, 0, slots, st));
   const bool refr = c->dev.any_transparent != 0, fc = c->dev.colour_fast != 0 && c->fast_clamp;
-  const unsigned resident = (unsigned)c->n_cu * 4u * RT_WAVES_PER_EU_WF;
-  const unsigned g0 = (unsigned)std::min<size_t>(n_tiles, resident), g1 = (unsigned)std::min<size_t>(cap / 64, resident);
+  uint32_t n_level[RT_MAX_DEPTH_CAP + 2] = {0};
+  n_level[0] = (uint32_t)slots;
+  int last = 0;
   for (int d = 0; d <= max_depth; ++d) {
-    const dim3 g(d == 0 ? g0 : g1);
-    if (refr && fc) hipLaunchKernelGGL((wf_trace_kernel<true, true>), g, dim3(64), 0, st, c->dev, A, d, a0, a1, a2, a3, max_depth);
-    else if (refr) hipLaunchKernelGGL((wf_trace_kernel<true, false>), g, dim3(64), 0, st, c->dev, A, d, a0, a1, a2, a3, max_depth);
-    else if (fc) hipLaunchKernelGGL((wf_trace_kernel<false, true>), g, dim3(64), 0, st, c->dev, A, d, a0, a1, a2, a3, max_depth);
-    else hipLaunchKernelGGL((wf_trace_kernel<false, false>), g, dim3(64), 0, st, c->dev, A, d, a0, a1, a2, a3, max_depth);
+    const uint32_t n = n_level[d];
+    if (n == 0) break;
+    last = d;
+    A.perm = nullptr;
+    if (d > 0) {                                             // this level's slots in key order
+      const WfLevel L = wf_level(A, d);                      // host-side pointer arithmetic only
+      size_t tb = sort_bytes;
+      RT_HIP(rt_wf_sort_pairs(tmp, &tb, L.key, kout, L.val, perm, (int)n, 30, st));
+      A.perm = perm;
+    }
+    const dim3 g((n + 63) / 64);
+    if (refr && fc) hipLaunchKernelGGL((wf_trace_kernel<true, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    else if (refr) hipLaunchKernelGGL((wf_trace_kernel<true, false>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    else if (fc) hipLaunchKernelGGL((wf_trace_kernel<false, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    else hipLaunchKernelGGL((wf_trace_kernel<false, false>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    RT_HIP(hipGetLastError());
+    if (d < max_depth) {
+      uint32_t cnt = 0;
+      RT_HIP(hipMemcpyAsync(&cnt, A.count + d + 1, 4, hipMemcpyDeviceToHost, st));
+      RT_HIP(hipStreamSynchronize(st));
+      n_level[d + 1] = std::min<uint32_t>(cnt, (uint32_t)cap);
+    }
   }
-  const dim3 gf((unsigned)c->n_cu * 8u), bf(256);
-  for (int d = max_depth; d >= 0; --d) {
-    if (f64 && fc) hipLaunchKernelGGL((wf_fold_kernel<true, true>), gf, bf, 0, st, c->dev, A, d, a0, a1, a2, a3, target, tstride, rgbi);
-    else if (f64) hipLaunchKernelGGL((wf_fold_kernel<true, false>), gf, bf, 0, st, c->dev, A, d, a0, a1, a2, a3, target, tstride, rgbi);
-    else if (fc) hipLaunchKernelGGL((wf_fold_kernel<false, true>), gf, bf, 0, st, c->dev, A, d, a0, a1, a2, a3, target, tstride, rgbi);
-    else hipLaunchKernelGGL((wf_fold_kernel<false, false>), gf, bf, 0, st, c->dev, A, d, a0, a1, a2, a3, target, tstride, rgbi);
+  const dim3 bf(256);
+  for (int d = last; d >= 0; --d) {
+    const uint32_t n = n_level[d];
+    const dim3 gf((n + 255) / 256);
+    if (f64 && fc) hipLaunchKernelGGL((wf_fold_kernel<true, true>), gf, bf, 0, st, c->dev, A, d, n, a0, a1, a2, a3, target, tstride, rgbi);
+    else if (f64) hipLaunchKernelGGL((wf_fold_kernel<true, false>), gf, bf, 0, st, c->dev, A, d, n, a0, a1, a2, a3, target, tstride, rgbi);
+    else if (fc) hipLaunchKernelGGL((wf_fold_kernel<false, true>), gf, bf, 0, st, c->dev, A, d, n, a0, a1, a2, a3, target, tstride, rgbi);
+    else hipLaunchKernelGGL((wf_fold_kernel<false, false>), gf, bf, 0, st, c->dev, A, d, n, a0, a1, a2, a3, target, tstride, rgbi);
   }
   const dim3 gx((unsigned)c->n_cu * 4u);
 #define RT_WF_FIX(R, F, FCv) hipLaunchKernelGGL((wf_fixup_kernel<R, F, FCv>), gx, dim3(64), 0, st, c->dev, A, a0, a1, a2, a3, max_depth, target, tstride, rgbi)
@@ -2464,8 +2560,10 @@ int rt_assemble_row_bands_rgb8(const uint8_t* gathered, size_t gathered_stride, 
   if (gathered_stride < (size_t)width * 3 || frame_stride < (size_t)width * 4) return fail(RT_ERR_INVALID, "row stride < row bytes");
   if ((((uintptr_t)frame) | frame_stride) & 3) return fail(RT_ERR_INVALID, "frame rows must be 4-byte aligned");
   if (!is_device_ptr(gathered) || !is_device_ptr(frame)) return fail(RT_ERR_INVALID, "frame assembly takes device pointers");
+  const bool vec = (width & 3) == 0 && (((uintptr_t)gathered | gathered_stride) & 3) == 0 &&
+                   (((uintptr_t)frame | frame_stride) & 15) == 0;
   hipLaunchKernelGGL(assemble_bands_rgb_kernel, dim3(height), dim3(256), 0, (hipStream_t)stream, gathered, gathered_stride,
-                     (int)world, (int)slot_rows, (int)band_rows, (int)width, frame, frame_stride);
+                     (int)world, (int)slot_rows, (int)band_rows, (int)width, frame, frame_stride, vec ? 1 : 0);
   RT_HIP(hipGetLastError());
   return RT_OK;
 }
