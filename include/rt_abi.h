@@ -250,14 +250,9 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  * compare/select form everywhere (A/B checks).
  * RT_OPT_WAVEFRONT_CAP: rays each recursion level of the wavefront path holds, in percent of the
  * launch's pixel slots (1..400, default 200); a pixel whose ray tree overflows a level is rendered
- * again by the per-lane megakernel (same bits), so the value trades memory against that fallback.
- * RT_OPT_DIVERGENT_WALK: -1 (default) auto, 1 on, 0 off.  On, secondary rays and their shadow rays
- * walk the object hierarchy per lane (vector loads) instead of wave-uniformly (scalar loads); auto
- * turns it on for scenes of >= 32 objects, where a wave of scattered rays would otherwise walk the
- * union of its lanes' paths.  Takes effect at the next upload or launch; drops the tile orders. */
+ * again by the per-lane megakernel (same bits), so the value trades memory against that fallback. */
 typedef enum rt_option {
-  RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4,
-  RT_OPT_DIVERGENT_WALK = 5
+  RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4
 } rt_option;
 typedef enum rt_kernel_choice {
   RT_KERNEL_AUTO = 0, RT_KERNEL_MEGA = 1, RT_KERNEL_DEFERRED = 2, RT_KERNEL_WAVEFRONT = 3

@@ -507,19 +507,13 @@ __device__ __forceinline__ bool obb_may_hit(const DS& S, cptr<RtObject> O, V3 ro
 // Both traversals walk the object hierarchy (RtTrav, pre-order over contiguous draw-order runs)
 // wave-coherently: `i` is uniform, a lane that misses a group resumes at its skip index, and the
 // wave jumps over a group no lane entered.  Objects are visited in draw order either way.
-// DIV (divergent walk): every lane walks its own path (`i` per lane, node / object / leaf records
-// read with per-lane vector loads).  The uniform walk visits the UNION of its lanes' paths: for
-// scattered secondary rays in a scene of many objects (fractal.scene: 171 objects, a ray meets ~7
-// leaves, its wave ~all 425) that is the whole scene, while a divergent wave costs its longest
-// lane's path.  Each lane still visits its objects in the same order, so every result is the
-// uniform walk's (first-visited-wins ties, the shadow product's order).
 
 // Nearest hit over all objects in draw order: accept d if d > EPS && d < nearest
 // (raytracer.rs:141-150).  The acceptance test is pure, so it runs BEFORE the (pure) CSG
 // filter: candidates that cannot win never pay for the sibling is_inside tests.
 // SHARE: concentric sphere leaves reuse their ray terms (SphereShare); it keeps three doubles live
 // across the leaf loop, so only kernels with register headroom take it (see trace()).
-template <bool SHARE = false, bool OBB = !SHARE, bool DIV = false>
+template <bool SHARE = false, bool OBB = !SHARE>
 __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0) {
   [[maybe_unused]] const int cb = cat * 9;
   CNT(cb + 0);
@@ -528,7 +522,7 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
   int bobj = -1;
   SphereShare shr = {0.0, 0.0, 0.0};
   const CullRay cr = cull_ray(ro, rd);
-  const bool fin = DIV ? finite3(ro) && finite3(rd) : wave_finite(ro, rd);
+  const bool fin = wave_finite(ro, rd);
   int resume = 0;
   // NORDER (reflection-only kernels): the objects in S.strav's order, largest regions first, so an
   // early hit on a big object culls what lies behind it.  Exact: a candidate equal to the best
@@ -539,16 +533,12 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
   const int n_tr = NORDER ? S.n_strav : S.n_trav;
   for (int i = 0; i < n_tr;) {
     cptr<RtTrav> T = &TR[i];
-    const bool act = DIV || i >= resume;
+    const bool act = i >= resume;
     if (T->obj < 0) {                                    // group node
       CNT(28 + cat);
       const bool in = act && box_may_hit(T->blo, T->bhi, cr, cull_tmax(best));
-      if constexpr (DIV) {
-        i = in ? i + 1 : T->skip;
-      } else {
-        if (act && !in) resume = T->skip;
-        i = __ballot(in) ? i + 1 : T->skip;
-      }
+      if (act && !in) resume = T->skip;
+      i = __ballot(in) ? i + 1 : T->skip;
       continue;
     }
     ++i;
@@ -596,7 +586,7 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
 // SORDER (reflection-only kernels): walk S.strav, the likeliest occluders first (scene.cpp
 // shadow_order) -- every transparency is +-0 there, so the first filtered hit decides and the
 // order is free.
-template <bool SHARE = false, bool OBB = !SHARE, bool SORDER = OBB, bool DIV = false>
+template <bool SHARE = false, bool OBB = !SHARE, bool SORDER = OBB>
 __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
   [[maybe_unused]] constexpr int cb = 18;
   CNT(cb + 0);
@@ -604,23 +594,19 @@ __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
   double tr = 1.0;
   SphereShare shr = {0.0, 0.0, 0.0};
   const CullRay cr = cull_ray(p, dir);
-  const bool fin = DIV ? finite3(p) && finite3(dir) : wave_finite(p, dir);
+  const bool fin = wave_finite(p, dir);
   const double tmax = cull_tmax(dist);
   int resume = 0;
   const cptr<RtTrav> TR = (RT_SHADOW_ORDER && SORDER) ? S.strav : S.trav;
   const int n_tr = (RT_SHADOW_ORDER && SORDER) ? S.n_strav : S.n_trav;
   for (int i = 0; i < n_tr;) {
     cptr<RtTrav> T = &TR[i];
-    const bool act = DIV || i >= resume;
+    const bool act = i >= resume;
     if (T->obj < 0) {                                    // group node
       CNT(30);
       const bool in = act && box_may_hit(T->blo, T->bhi, cr, tmax);
-      if constexpr (DIV) {
-        i = in ? i + 1 : T->skip;
-      } else {
-        if (act && !in) resume = T->skip;
-        i = __ballot(in) ? i + 1 : T->skip;
-      }
+      if (act && !in) resume = T->skip;
+      i = __ballot(in) ? i + 1 : T->skip;
       continue;
     }
     ++i;
@@ -834,10 +820,6 @@ typedef LDS_AS double lds_f64;
 #ifndef RT_LDS_FRAMES
 #define RT_LDS_FRAMES 2
 #endif
-// Refraction-chain kernels (RT_MODE_CHAIN): frames of the chain stack kept in LDS.
-#ifndef RT_LDS_FRAMES_CHAIN
-#define RT_LDS_FRAMES_CHAIN RT_LDS_FRAMES
-#endif
 // Refraction frames also carry the pending reflection ray (P, D, rp: 7 doubles); the first
 // KLR of them go to LDS after the KL colour frames, [frame][component][lane] likewise.
 #ifndef RT_LDS_RFRAMES
@@ -850,9 +832,7 @@ typedef LDS_AS double lds_f64;
 // KLR > 0 (REFR): the pending-reflection state of frames 0..KLR-1 at lf[(KL * 4 + f * 7 + c) * 64].
 // CHAIN (REFR scenes with RtDevScene::ray_chains): every hit spawns at most one ray, so a refraction
 // frame never carries a pending reflection: frames are (A, w) as in the reflection-only kernels.
-// DIV: secondary rays (depth >= 1) and their shadow rays take the divergent walk (see nearest_hit);
-// primary rays and their shadows stay on the uniform walk (coherent: one 8x8 tile per wave).
-template <bool REFR, class Rec = NoRec, int KL = 0, bool FC = false, int KLR = 0, bool CHAIN = false, bool DIV = false>
+template <bool REFR, class Rec = NoRec, int KL = 0, bool FC = false, int KLR = 0, bool CHAIN = false>
 __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, lds_f64* lf = nullptr) {
   double fA[RT_MAX_DEPTH_CAP][3];     // parent colour already intensified by (1 - w)
   double fW[RT_MAX_DEPTH_CAP];        // child weight w (transparency or reflectivity)
@@ -907,9 +887,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
     bool descend = false;
     double t_hit;
     PROF_T0(p0);
-    const bool sec = trip != 0;                           // wave-uniform: active lanes iterate together
-    const int oi = DIV && sec ? nearest_hit<SHARE, OBB, true>(S, ro, rd, &t_hit, 1)
-                              : nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit, trip == 0 ? 0 : 1);
+    const int oi = nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit, trip == 0 ? 0 : 1);
     PROF_ADD(trip == 0 ? 0 : 1, p0);
     ++trip;
     PROF_T0(p1);
@@ -941,8 +919,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
         const double t = lv.x > 1e300 ? 0.5 : 1.0;
 #else
         PROF_T0(p2);
-        const double t = DIV && sec ? shadow_transparency<SHARE, OBB, OBB, true>(S, p, sdir, ll)   // :176-197
-                                    : shadow_transparency<SHARE, OBB>(S, p, sdir, ll);
+        const double t = shadow_transparency<SHARE, OBB>(S, p, sdir, ll);       // :176-197
         PROF_ADD(2, p2);
 #endif
         if (!have_shading) {
@@ -1255,7 +1232,6 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
 #define RT_MODE_REFL 0
 #define RT_MODE_CHAIN 1
 #define RT_MODE_TREE 2
-#define RT_MODE_DIV 8          // flag: secondary rays take the divergent walk (RtDevScene::div_walk)
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 4
 #endif
@@ -1266,7 +1242,7 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
 #define RT_WAVES_PER_EU_CHAIN 5
 #endif
 #define RT_WAVES(REFR) ((REFR) ? RT_WAVES_PER_EU : RT_WAVES_PER_EU_NOREFR)
-#define RT_WAVES_MODE(M) (((M) & 7) == RT_MODE_REFL ? RT_WAVES_PER_EU_NOREFR : ((M) & 7) == RT_MODE_CHAIN ? RT_WAVES_PER_EU_CHAIN : RT_WAVES_PER_EU)
+#define RT_WAVES_MODE(M) ((M) == RT_MODE_REFL ? RT_WAVES_PER_EU_NOREFR : (M) == RT_MODE_CHAIN ? RT_WAVES_PER_EU_CHAIN : RT_WAVES_PER_EU)
 // Workgroup = one wave of 8x8 pixels: measured 3-5 % faster than 2x2-wave workgroups (round 1).
 constexpr int RT_WG_THREADS = 64;
 constexpr int RT_TILE_W = 8, RT_TILE_H = 8;
@@ -1275,7 +1251,7 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
                                                           int n_rows, int max_depth, uint8_t* __restrict__ out,
                                                           size_t stride, const int32_t* __restrict__ order,
                                                           uint32_t* __restrict__ cost, int rgb) {
-  constexpr bool REFR = (MODE & 7) != RT_MODE_REFL, CHAIN = (MODE & 7) == RT_MODE_CHAIN, DIV = (MODE & RT_MODE_DIV) != 0;
+  constexpr bool REFR = MODE != RT_MODE_REFL, CHAIN = MODE == RT_MODE_CHAIN;
 #ifdef RT_DIAG_LDS                       // diagnostic builds only: cap occupancy with an LDS pad
   __shared__ volatile char rt_pad[RT_DIAG_LDS];
   if (threadIdx.x == 0) rt_pad[0] = 0;
@@ -1298,13 +1274,12 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   PROF_T0(p5);
   camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
 #if RT_LDS_FRAMES > 0
-  constexpr int KLR = (MODE & 7) == RT_MODE_TREE ? RT_LDS_RFRAMES : 0;
-  constexpr int KL = CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES;
-  __shared__ double s_frames[(KL * 4 + KLR * 7) * 64];   // frame stack, see trace()
+  constexpr int KLR = MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0;
+  __shared__ double s_frames[(RT_LDS_FRAMES * 4 + KLR * 7) * 64];   // frame stack, see trace()
   lds_f64* lf = (lds_f64*)&s_frames[lane];
-  const Col c = trace<REFR, NoRec, KL, FC, KLR, CHAIN, DIV>(make_ds(S), ro, rd, max_depth, nullptr, lf);
+  const Col c = trace<REFR, NoRec, RT_LDS_FRAMES, FC, KLR, CHAIN>(make_ds(S), ro, rd, max_depth, nullptr, lf);
 #else
-  const Col c = trace<REFR, NoRec, 0, FC, 0, CHAIN, DIV>(make_ds(S), ro, rd, max_depth);
+  const Col c = trace<REFR, NoRec, 0, FC, 0, CHAIN>(make_ds(S), ro, rd, max_depth);
 #endif
   PROF_ADD(5, p5);
   uint8_t* row = out + (size_t)r * stride;
@@ -2012,8 +1987,6 @@ struct rt_ctx {
   bool tile_order = true;               // rt_ctx_set_option(RT_OPT_TILE_ORDER): cost-ordered dispatch
   bool fast_clamp = true;               // rt_ctx_set_option(RT_OPT_FAST_CLAMP): min/max clamps where exact
   int wf_cap_pct = 200;                 // rt_ctx_set_option(RT_OPT_WAVEFRONT_CAP): rays per level, % of pixel slots
-  int div_opt = -1;                     // rt_ctx_set_option(RT_OPT_DIVERGENT_WALK): -1 auto, 0 off, 1 on
-  bool div_walk = false;                // this scene's secondary rays take the divergent walk
   double wf_klo[3] = {-100, -100, -100}, wf_khi[3] = {100, 100, 100};   // coherence-key extent (bounded objects)
   int n_cu = 256;                       // compute units of the device (wave slots = n_cu x 4 SIMDs x waves/SIMD)
   bool uploaded = false;
@@ -2071,11 +2044,6 @@ using rt::fail;
 // is 7-20 % faster.  The deferred kernel's order entries hold the tile index in 20 bits
 // (RT_SPLIT_TILE_MASK), so launches of more tiles always take the megakernel.
 #define RT_DEFERRED_MAX_TILES 40000
-// Scenes of at least this many objects send their secondary rays down the divergent walk (DIV): a
-// wave of scattered rays then costs its longest lane's path instead of the union of its lanes'.
-#ifndef RT_DIV_MIN_OBJECTS
-#define RT_DIV_MIN_OBJECTS 32
-#endif
 
 static void drop_order(rt_ctx::OrderSlot& s) {
   if (s.d_order) (void)hipFree(s.d_order);     // hipFree waits for work that may still read it
@@ -2223,7 +2191,6 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   d.ray_chains = f.ray_chains;
   d.cam = f.cam;
   c->max_depth = f.max_depth;
-  c->div_walk = c->div_opt == 1 || (c->div_opt == -1 && (int)f.objects.size() >= RT_DIV_MIN_OBJECTS);
   {                                   // the wavefront path's key extent: the hull of the bounded objects
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (const RtObject& o : f.objects)
@@ -2444,21 +2411,14 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   else hipLaunchKernelGGL((render_rows_deferred_kernel<F, false, false, R>), grid, dim3(64), 0, st, c->dev, a0, a1,  \
                           a2, a3, max_depth, target, tstride, order, cost, rgbi);
   const bool fc = c->dev.colour_fast != 0 && c->fast_clamp;
-  const bool div = c->div_walk;
   if (deferred && chain && f64) { RT_LAUNCH_DEFERRED(true, true) }
   else if (deferred && chain) { RT_LAUNCH_DEFERRED(false, true) }
-  else if (chain && div && f64) { RT_LAUNCH_ROWS(RT_MODE_CHAIN | RT_MODE_DIV, true) }
-  else if (chain && div) { RT_LAUNCH_ROWS(RT_MODE_CHAIN | RT_MODE_DIV, false) }
   else if (chain && f64) { RT_LAUNCH_ROWS(RT_MODE_CHAIN, true) }
   else if (chain) { RT_LAUNCH_ROWS(RT_MODE_CHAIN, false) }
-  else if (refr && div && f64) { RT_LAUNCH_ROWS(RT_MODE_TREE | RT_MODE_DIV, true) }
-  else if (refr && div) { RT_LAUNCH_ROWS(RT_MODE_TREE | RT_MODE_DIV, false) }
   else if (refr && f64) { RT_LAUNCH_ROWS(RT_MODE_TREE, true) }
   else if (refr) { RT_LAUNCH_ROWS(RT_MODE_TREE, false) }
   else if (deferred && f64) { RT_LAUNCH_DEFERRED(true, false) }
   else if (deferred) { RT_LAUNCH_DEFERRED(false, false) }
-  else if (div && f64) { RT_LAUNCH_ROWS(RT_MODE_REFL | RT_MODE_DIV, true) }
-  else if (div) { RT_LAUNCH_ROWS(RT_MODE_REFL | RT_MODE_DIV, false) }
   else if (f64) { RT_LAUNCH_ROWS(RT_MODE_REFL, true) }
   else { RT_LAUNCH_ROWS(RT_MODE_REFL, false) }
 #undef RT_LAUNCH_ROWS
@@ -2846,16 +2806,6 @@ int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
     if (value != 0 && value != 1) return fail(RT_ERR_INVALID, "RT_OPT_TIMING value %d", value);
     c->timing = value != 0;
     c->timed = false;                  // no launch recorded under the new setting yet
-    return RT_OK;
-  }
-  if (option == RT_OPT_DIVERGENT_WALK) {
-    if (value < -1 || value > 1) return fail(RT_ERR_INVALID, "RT_OPT_DIVERGENT_WALK %d not in [-1, 1]", value);
-    if (value != c->div_opt) {
-      RT_HIP(hipSetDevice(c->device));
-      drop_orders(c);                 // tile costs were measured with the other walk
-      c->div_opt = value;
-      if (c->uploaded) c->div_walk = value == 1 || (value == -1 && c->dev.n_objects >= RT_DIV_MIN_OBJECTS);
-    }
     return RT_OK;
   }
   if (option == RT_OPT_WAVEFRONT_CAP) {

@@ -302,12 +302,6 @@ class Renderer:
         percent of the launch's pixel slots (pixels whose tree overflows are re-rendered, same bits)."""
         check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_WAVEFRONT_CAP, int(percent)))
 
-    def set_divergent_walk(self, mode) -> None:
-        """rt_ctx_set_option(RT_OPT_DIVERGENT_WALK): "auto" (scenes of >= 32 objects), True or False --
-        secondary rays walk the object hierarchy per lane (same pixels)."""
-        v = -1 if mode == "auto" else (1 if mode else 0)
-        check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_DIVERGENT_WALK, v))
-
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()
         check(lib().rt_ctx_last_kernel_ms(self.h, ctypes.byref(ms)))

@@ -24,10 +24,7 @@ for d in depths:
         rt.max_depth = d
         rt.load_scene(text, t, asset_dir=S)
         r = rt.renderer
-        kern, _, opt = k.partition(":")           # e.g. mega:div0 / mega:div1 (RT_OPT_DIVERGENT_WALK)
-        r.set_kernel(kern)
-        if opt:
-            r.set_divergent_walk({"div0": False, "div1": True, "divauto": "auto"}[opt])
+        r.set_kernel(k)
         out = r.render_rows(0, H)
         torch.cuda.synchronize()
         cal = r.last_kernel_ms()
