@@ -95,3 +95,19 @@ def test_wavefront_option_bounds():
     for bad in (0, 401):
         with pytest.raises(T.RtError):
             rt.renderer.set_wavefront_cap(bad)
+
+
+@pytest.mark.parametrize("name,t", [("fractal", 0.0), ("fractal", 0.5)])
+def test_ray_tree_autotune_same_pixels(worldmap, name, t):
+    """Ray-tree scenes under RT_KERNEL_AUTO: the calibration launch, the first ordered launch (timed
+    against one wavefront launch of the same rows) and the launches after it (whichever path won)
+    all give the oracle's pixels."""
+    import tinyraytracerinrust_amd as T
+    from oracle import oracle as O
+    W, H = 640, 480                                  # 4800 tiles: calibrated, ordered, autotuned
+    rt = T.RayTracer(W, H)
+    rt.load_scene(scene_text(name), t, asset_dir=SCENES)
+    frames = [rt.renderer.render_rows_host(0, H) for _ in range(4)]
+    _, ru = O.OracleScene(scene_text(name), t, W, H).render(0, H)
+    for k, f in enumerate(frames):
+        assert_close(f, None, ru, None, f"{name} t={t} auto launch {k}")

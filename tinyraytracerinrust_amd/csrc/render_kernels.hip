@@ -820,6 +820,10 @@ typedef LDS_AS double lds_f64;
 #ifndef RT_LDS_FRAMES
 #define RT_LDS_FRAMES 2
 #endif
+// Refraction-chain kernels (RT_MODE_CHAIN): frames of the chain stack kept in LDS.
+#ifndef RT_LDS_FRAMES_CHAIN
+#define RT_LDS_FRAMES_CHAIN RT_LDS_FRAMES
+#endif
 // Refraction frames also carry the pending reflection ray (P, D, rp: 7 doubles); the first
 // KLR of them go to LDS after the KL colour frames, [frame][component][lane] likewise.
 #ifndef RT_LDS_RFRAMES
@@ -1275,9 +1279,10 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
 #if RT_LDS_FRAMES > 0
   constexpr int KLR = MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0;
-  __shared__ double s_frames[(RT_LDS_FRAMES * 4 + KLR * 7) * 64];   // frame stack, see trace()
+  constexpr int KL = CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES;
+  __shared__ double s_frames[(KL * 4 + KLR * 7) * 64];   // frame stack, see trace()
   lds_f64* lf = (lds_f64*)&s_frames[lane];
-  const Col c = trace<REFR, NoRec, RT_LDS_FRAMES, FC, KLR, CHAIN>(make_ds(S), ro, rd, max_depth, nullptr, lf);
+  const Col c = trace<REFR, NoRec, KL, FC, KLR, CHAIN>(make_ds(S), ro, rd, max_depth, nullptr, lf);
 #else
   const Col c = trace<REFR, NoRec, 0, FC, 0, CHAIN>(make_ds(S), ro, rd, max_depth);
 #endif
@@ -1991,6 +1996,7 @@ struct rt_ctx {
   int n_cu = 256;                       // compute units of the device (wave slots = n_cu x 4 SIMDs x waves/SIMD)
   bool uploaded = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t tev0 = nullptr, tev1 = nullptr;   // the wavefront autotune's own pair
   bool timed = false;
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -2011,6 +2017,7 @@ struct rt_ctx {
     uint32_t grid = 0;                // entries of the order (> n_tiles when costly tiles are split)
     uint64_t last_use = 0;
     bool deferred = false;            // ordered launches take the deferred-shadow kernel
+    int wf_tune = 0;                  // ray-tree scenes, RT_KERNEL_AUTO: 0 not yet timed, 1 megakernel, 2 wavefront
     bool valid = false;               // set once the sorted order is on the device
   };
   static constexpr int RT_ORDER_SLOTS = 8;
@@ -2142,7 +2149,8 @@ int rt_ctx_create(int device, rt_ctx** out) {
   c->device = device;
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   memset(&c->dev, 0, sizeof c->dev);
-  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->tev0) != hipSuccess || hipEventCreate(&c->tev1) != hipSuccess) {
     delete c;
     return fail(RT_ERR_DEVICE, "stream/event creation failed");
   }
@@ -2411,6 +2419,24 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   else hipLaunchKernelGGL((render_rows_deferred_kernel<F, false, false, R>), grid, dim3(64), 0, st, c->dev, a0, a1,  \
                           a2, a3, max_depth, target, tstride, order, cost, rgbi);
   const bool fc = c->dev.colour_fast != 0 && c->fast_clamp;
+  // Ray-tree scenes (a transparent AND reflective object) under RT_KERNEL_AUTO: the first ordered
+  // launch of a geometry is timed against one wavefront launch of the same rows, and the faster
+  // path takes every later launch (fractal.scene 1080p: 16.4 vs 25.9 ms, profiles/r03d_timing.txt;
+  // the small ray-tree scenes of the fuzz suite mostly keep the megakernel).  Same pixels either way.
+  const bool tree = refr && !chain;
+  if (order && tree && slot->wf_tune == 2) {
+    int rc = launch_wavefront(c, st, a0, a1, a2, a3, max_depth, target, tstride, f64, rgbi, n_tiles);
+    if (rc) return rc;
+    if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
+    c->timed = c->timing;
+    if (!dev_out) {
+      RT_HIP(hipMemcpy2DAsync(out, stride, target, tstride, row_bytes, n_rows, hipMemcpyDeviceToHost, st));
+      RT_HIP(hipStreamSynchronize(st));
+    }
+    return RT_OK;
+  }
+  const bool tune = order && tree && dmode == -1 && slot->wf_tune == 0;
+  if (tune) RT_HIP(hipEventRecord(c->tev0, st));
   if (deferred && chain && f64) { RT_LAUNCH_DEFERRED(true, true) }
   else if (deferred && chain) { RT_LAUNCH_DEFERRED(false, true) }
   else if (chain && f64) { RT_LAUNCH_ROWS(RT_MODE_CHAIN, true) }
@@ -2426,6 +2452,23 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   RT_HIP(hipGetLastError());
   if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
   c->timed = c->timing;
+  if (tune) {                         // synchronous, once per ray-tree geometry (see above)
+    float mega_ms = 0.0f, wf_ms = 0.0f;
+    RT_HIP(hipEventRecord(c->tev1, st));
+    RT_HIP(hipEventSynchronize(c->tev1));
+    RT_HIP(hipEventElapsedTime(&mega_ms, c->tev0, c->tev1));
+    RT_HIP(hipEventRecord(c->tev0, st));
+    int rc = launch_wavefront(c, st, a0, a1, a2, a3, max_depth, target, tstride, f64, rgbi, n_tiles);
+    if (rc) return rc;
+    RT_HIP(hipEventRecord(c->tev1, st));
+    RT_HIP(hipEventSynchronize(c->tev1));
+    RT_HIP(hipEventElapsedTime(&wf_ms, c->tev0, c->tev1));
+    slot->wf_tune = wf_ms < mega_ms ? 2 : 1;
+    static const bool order_debug = getenv("RT_TILE_ORDER_DEBUG") != nullptr;
+    if (order_debug)
+      fprintf(stderr, "ray-tree autotune: megakernel %.3f ms, wavefront %.3f ms -> %s\n", mega_ms, wf_ms,
+              slot->wf_tune == 2 ? "wavefront" : "megakernel");
+  }
   if (calibrate) {                    // synchronous, once per geometry and scene upload
     std::vector<uint32_t> h_cost(n_tiles);
     std::vector<int32_t> h_order(n_tiles);
@@ -2876,6 +2919,8 @@ void rt_ctx_free(rt_ctx* c) {
   drop_orders(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->tev0) (void)hipEventDestroy(c->tev0);
+  if (c->tev1) (void)hipEventDestroy(c->tev1);
   delete c;
 }
 
