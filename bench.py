@@ -876,7 +876,7 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
             "unit": "TFLOP/s",
             "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4) if achieved else None,
             "traffic": load_traffic(a.config, 1, "contiguous"),     # HBM bytes per frame (PMC, profiles/)
-            "kernel": "render_rows_kernel<RT_MODE_CHAIN> or render_rows_deferred_kernel<REFR> (RT_OPT_KERNEL " + a.kernel + ")",
+            "kernel": "render_rows_kernel<RT_MODE_CHAIN> (ray-chain scene; RT_OPT_KERNEL " + a.kernel + ")",
             "streams": K,
             "achieved_basis": "kernel event time" if K == 1 else "step wall time (frames overlap on the streams)",
             "kernel_ms_mean": round(sum(per_frame) / len(per_frame), 4),

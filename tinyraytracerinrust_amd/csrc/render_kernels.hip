@@ -1265,6 +1265,9 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   // measured on a calibration launch that stored each tile's wave time in `cost`.
   // CAL (the calibration instantiation) is the only one that carries the timing code.
   const unsigned tile = CAL || !order ? blockIdx.x : (unsigned)order[blockIdx.x];
+#ifdef RT_DIAG_HOT_TILES                 // diagnostic A/B builds only: issue priority for the costliest tiles
+  if (!CAL && order && blockIdx.x < RT_DIAG_HOT_TILES) __builtin_amdgcn_s_setprio(3);
+#endif
   [[maybe_unused]] uint64_t t_start = 0;
   if constexpr (CAL) t_start = wall_clock64();
   const unsigned tiles_x = (unsigned)(S.width + RT_TILE_W - 1) / RT_TILE_W;
