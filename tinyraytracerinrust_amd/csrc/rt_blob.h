@@ -52,37 +52,42 @@ struct RtProg { int32_t op, arg; };
 #define RT_XF_IDENTITY 2   // RtLeaf::xdiag value of an identity inverse (a diagonal-affine special case)
 
 struct alignas(16) RtLeaf {
+  // Field order = access order of a traversal's leaf evaluation (the kernels read these through
+  // scalar loads, 64-byte scalar-cache lines): the integer header and the culling box, then the
+  // inverse transform, then the primitive's parameters; the shading-only fields (forward matrix,
+  // surface tests, quirk planes) last.
+  int32_t kind;         // RtNodeKind (leaf kinds only)
+  int32_t cull;         // RtCull
+  int32_t xdiag;        // 1: inv is diagonal-affine (see below): transform_vector has a 2-op form;
+                        // RT_XF_IDENTITY: inv is the identity and inv_o = 0: no transform at all
+  int32_t share_prev;   // sphere leaf: 1 = the previous leaf of the object is a sphere with a bit-identical
+                        // inverse transform (inv, inv_o, xdiag) and centre, and every traversal that
+                        // evaluates this leaf has evaluated that one first (see below)
+  int32_t plane_axis;   // untransformed plane leaf: 0/1/2 when pnorm has exactly one nonzero (finite) component; else -1
+  int32_t filter_const; // 1: every literal of the hit filter passes for any hit of this leaf whose ray origin is
+                        // within 1e6 (concentric spheres under one transform, radii apart by more than the
+                        // rounding margin: scene.cpp const_filters), so the traversals skip the filter
+  int32_t prog_begin;   // hit-filter program [prog_begin, prog_end)
+  int32_t prog_end;
+  int32_t n_lit;        // >= 0: the filter program is the conjunction of n_lit literals below
+  int32_t lit[RT_MAX_LITS];   // literal = 2 * leaf + want: leaf[lit >> 1].is_inside(p) == (lit & 1)
+  int32_t pad0[3];
+  double blo[3], bhi[3];// culling box of this leaf's accepted hits (own bound ^ required-inside siblings)
   double inv[12];       // inverse matrix rows 0..2 (row-major, 4 per row)
   double inv_o[3];      // transform_vector((0,0,0), inverse)   (transformation.rs:80-83)
-  double mat[12];       // forward matrix rows 0..2
-  double mat_o[3];      // transform_vector((0,0,0), matrix)    (transformation.rs:71-74)
   double c[3];          // sphere / cube centre
   double radius;        // sphere radius | cube half length ("length", math_shapes.rs:229)
   double r2;            // sphere: radius * radius
   double r_eps;         // sphere: radius + EPSILON
   double lo[3];         // cube: centre - length
   double hi[3];         // cube: centre + length
+  double pnorm[3];      // plane leaf: Vector::new(a,b,c).normalized() (math_shapes.rs:169)
+  double pl[6][4];      // plane leaf: pl[0] = raw (a,b,c,d); cube: p1..p6 raw (a,b,c,d)
   double lo_e[3];       // cube: centre - length - EPSILON
   double hi_e[3];       // cube: centre + length + EPSILON
-  double pl[6][4];      // plane leaf: pl[0] = raw (a,b,c,d); cube: p1..p6 raw (a,b,c,d)
+  double mat[12];       // forward matrix rows 0..2
+  double mat_o[3];      // transform_vector((0,0,0), matrix)    (transformation.rs:71-74)
   double pn[6][3];      // matching transformed unit normals (MathPlane::normal)
-  double pnorm[3];      // plane leaf: Vector::new(a,b,c).normalized() (math_shapes.rs:169)
-  double blo[3], bhi[3];// culling box of this leaf's accepted hits (own bound ^ required-inside siblings)
-  int32_t kind;         // RtNodeKind (leaf kinds only)
-  int32_t prog_begin;   // hit-filter program [prog_begin, prog_end)
-  int32_t prog_end;
-  int32_t cull;         // RtCull
-  int32_t xdiag;        // 1: inv is diagonal-affine (see below): transform_vector has a 2-op form;
-                        // RT_XF_IDENTITY: inv is the identity and inv_o = 0: no transform at all
-  int32_t n_lit;        // >= 0: the filter program is the conjunction of n_lit literals below
-  int32_t lit[RT_MAX_LITS];   // literal = 2 * leaf + want: leaf[lit >> 1].is_inside(p) == (lit & 1)
-  int32_t plane_axis;   // untransformed plane leaf: 0/1/2 when pnorm has exactly one nonzero (finite) component; else -1
-  int32_t filter_const; // 1: every literal of the hit filter passes for any hit of this leaf whose ray origin is
-                        // within 1e6 (concentric spheres under one transform, radii apart by more than the
-                        // rounding margin: scene.cpp const_filters), so the traversals skip the filter
-  int32_t share_prev;   // sphere leaf: 1 = the previous leaf of the object is a sphere with a bit-identical
-                        // inverse transform (inv, inv_o, xdiag) and centre, and every traversal that
-                        // evaluates this leaf has evaluated that one first (see below)
 };
 // share_prev: the traversals evaluate an object's leaves in order, each unless its own box test
 // culls it (only when the object has leaf_cull).  The host sets share_prev only if the previous
