@@ -250,13 +250,9 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  * compare/select form everywhere (A/B checks).
  * RT_OPT_WAVEFRONT_CAP: rays each recursion level of the wavefront path holds, in percent of the
  * launch's pixel slots (1..400, default 200); a pixel whose ray tree overflows a level is rendered
- * again by the per-lane megakernel (same bits), so the value trades memory against that fallback.
- * RT_OPT_WAVEFRONT_GROUP: lanes per ray on the wavefront path's levels >= 1 (1, 4 or 8, default 8):
- * the lanes of a ray split the scene's objects, so a wave of 64 / G scattered rays no longer walks
- * the union of 64 rays' paths (same pixels). */
+ * again by the per-lane megakernel (same bits), so the value trades memory against that fallback. */
 typedef enum rt_option {
-  RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4,
-  RT_OPT_WAVEFRONT_GROUP = 5
+  RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4
 } rt_option;
 typedef enum rt_kernel_choice {
   RT_KERNEL_AUTO = 0, RT_KERNEL_MEGA = 1, RT_KERNEL_DEFERRED = 2, RT_KERNEL_WAVEFRONT = 3

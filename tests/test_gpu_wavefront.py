@@ -19,7 +19,7 @@ CASES = [("globes", 0.0, 160, 120, 10), ("globes", 0.25, 640, 480, 10), ("globes
          ("spinning_gimbals", 0.4, 160, 120, 10), ("fractal", 0.0, 160, 120, 10), ("fractal", 0.0, 96, 72, 2)]
 
 
-def _render(text, t, W, H, d, cap=None, rows=None, group=None):
+def _render(text, t, W, H, d, cap=None, rows=None):
     import tinyraytracerinrust_amd as T
     rt = T.RayTracer(W, H)
     rt.max_depth = d
@@ -28,8 +28,6 @@ def _render(text, t, W, H, d, cap=None, rows=None, group=None):
     r.set_kernel("wavefront")
     if cap is not None:
         r.set_wavefront_cap(cap)
-    if group is not None:
-        r.set_wavefront_group(group)
     y0, y1 = rows or (0, H)
     return r.render_rows_host(y0, y1), r.render_rows_host(y0, y1, f64=True)
 
@@ -97,9 +95,6 @@ def test_wavefront_option_bounds():
     for bad in (0, 401):
         with pytest.raises(T.RtError):
             rt.renderer.set_wavefront_cap(bad)
-    for bad in (0, 2, 16):
-        with pytest.raises(T.RtError):
-            rt.renderer.set_wavefront_group(bad)
 
 
 @pytest.mark.parametrize("name,t", [("fractal", 0.0), ("fractal", 0.5)])
@@ -116,27 +111,3 @@ def test_ray_tree_autotune_same_pixels(worldmap, name, t):
     _, ru = O.OracleScene(scene_text(name), t, W, H).render(0, H)
     for k, f in enumerate(frames):
         assert_close(f, None, ru, None, f"{name} t={t} auto launch {k}")
-
-
-@pytest.mark.parametrize("group", [1, 4, 8])
-@pytest.mark.parametrize("name,t,W,H,d", [("fractal", 0.0, 160, 120, 10), ("globes", 0.25, 160, 120, 10),
-                                          ("spinning_globes", 0.3, 160, 120, 10), ("three_cubes", 0.0, 96, 72, 10),
-                                          ("spinning_gimbals", 0.4, 96, 72, 10)])
-def test_wavefront_ray_groups(worldmap, group, name, t, W, H, d):
-    """Cooperative ray groups (RT_OPT_WAVEFRONT_GROUP: the G lanes of a ray split the objects; nearest
-    hit by (t, draw index) reduction, shadow products zero / one / the first lane's exact walk)."""
-    from oracle import oracle as O
-    gu, gf = _render(scene_text(name), t, W, H, d, group=group)
-    rf, ru = O.OracleScene(scene_text(name), t, W, H, max_depth=d).render(0, H, f64=True)
-    assert_close(gu, gf, ru, rf, f"wavefront G={group} {name}")
-
-
-@pytest.mark.parametrize("seed", range(7000, 7024))
-def test_wavefront_ray_groups_random_scenes(seed):
-    from tests.scene_fuzz import random_scene
-    from oracle import oracle as O
-    text = random_scene(seed, chains=seed % 2 == 0)
-    W, H, d = 96, 72, 6
-    gu, gf = _render(text, 0.0, W, H, d, group=4 if seed % 3 == 0 else 8)
-    rf, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H, f64=True)
-    assert_close(gu, gf, ru, rf, f"wavefront groups random scene {seed}")

@@ -1448,127 +1448,17 @@ __device__ __forceinline__ uint32_t wf_key(const WfArena& A, V3 o, V3 d) {
          (wf_spread9(cell(o.z, A.klo[2], A.kscale[2])) << 2);
 }
 
-// ---- cooperative ray groups (G lanes per ray) for the wavefront path's secondary levels
-// A wave of 64 scattered rays walking the object hierarchy wave-coherently visits the UNION of its
-// lanes' paths; with few waves in flight nothing hides that latency (fractal.scene: every level ~1
-// ms, profiles/r03e_kt_stats.csv).  Here a wave holds 64 / G rays, and the G lanes of a ray split the
-// objects: lane `gsub` takes objects gsub, gsub + G, sub + 2G, ... (a flat walk, the object's own box
-// and oriented box, then its leaves), so a wave issues each chunk of G objects for its 64 / G rays at
-// once.  Exactness:
-//   nearest hit: every lane keeps the best (t, object) of its objects (strict <, objects ascending),
-//     the group takes the minimum t and, on equal t, the lowest object index -- the reference's
-//     first-visited-wins over draw order (raytracer.rs:141-150), as the NORDER walk's tie rule;
-//   shadow rays: the product of the filtered hits' transparencies in draw order (:181-197) is +-0 as
-//     soon as one factor is 0 (every transparency finite: RtDevScene::shadow_early_out), 1 when there
-//     is no factor other than transparency-1.0 objects', and otherwise the group's first lane walks
-//     the objects in draw order itself (the uniform walk of shadow_transparency).  A zero of either
-//     sign is `t == 0` to every consumer (the light is skipped, raytracer.rs:199-200).
-template <int G>
-__device__ __forceinline__ int coop_reduce_nearest(double* t, int o) {
-#pragma unroll
-  for (int m = 1; m < G; m <<= 1) {
-    const double t2 = __shfl_xor(*t, m);
-    const int o2 = __shfl_xor(o, m);
-    if (t2 < *t || (t2 == *t && o2 >= 0 && (o < 0 || o2 < o))) { *t = t2; o = o2; }
-  }
-  return o;
-}
-template <int G>
-__device__ __forceinline__ bool coop_any(bool v) {
-  int x = v ? 1 : 0;
-#pragma unroll
-  for (int m = 1; m < G; m <<= 1) x |= __shfl_xor(x, m);
-  return x != 0;
-}
-
-template <bool SHARE, int G>
-__device__ int nearest_hit_coop(const DS& S, V3 ro, V3 rd, int gsub, double* dist) {
-  double best = INFINITY;
-  int bobj = -1;
-  SphereShare shr = {0.0, 0.0, 0.0};
-  const CullRay cr = cull_ray(ro, rd);
-  const bool fin = finite3(ro) && finite3(rd);
-  for (int o0 = 0; o0 < S.n_objects; o0 += G) {
-    const int o = o0 + gsub;
-    if (o >= S.n_objects) continue;
-    cptr<RtObject> O = &S.objects[o];
-    if (O->cull == RT_CULL_ALWAYS) continue;
-    if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, cr, cull_tmax(best))) continue;
-    if (RT_OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, ro, rd, cull_tmax(best))) continue;
-    const int lb = O->leaf_begin, le = lb + O->leaf_count;
-    for (int l = lb; l < le; ++l) {
-      cptr<RtLeaf> L = &S.leaves[l];
-      if (O->leaf_cull) {
-        if (L->cull == RT_CULL_ALWAYS) continue;
-        if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, cull_tmax(best))) continue;
-      }
-      double t0 = 0.0, t1 = 0.0;
-      const int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1, SHARE ? &shr : nullptr);
-      const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && SHARE && L->filter_const && !isnan(cr.inv.x));
-      if (n >= 1 && t0 > EPS && t0 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) { best = t0; bobj = o; }
-      if (n >= 2 && t1 > EPS && t1 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t1))))) { best = t1; bobj = o; }
-    }
-  }
-  bobj = coop_reduce_nearest<G>(&best, bobj);
-  *dist = best;
-  return bobj;
-}
-
-template <bool SHARE, int G>
-__device__ double shadow_transparency_coop(const DS& S, V3 p, V3 dir, double dist, int gsub) {
-  const CullRay cr = cull_ray(p, dir);
-  const bool fin = finite3(p) && finite3(dir);
-  const double tmax = cull_tmax(dist);
-  bool zero = false, other = false;
-  SphereShare shr = {0.0, 0.0, 0.0};
-  for (int o0 = 0; o0 < S.n_objects && !zero; o0 += G) {
-    const int o = o0 + gsub;
-    if (o >= S.n_objects) continue;
-    cptr<RtObject> O = &S.objects[o];
-    if (O->shadow_skip || O->cull == RT_CULL_ALWAYS) continue;
-    if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, cr, tmax)) continue;
-    if (RT_OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, p, dir, tmax)) continue;
-    const double tobj = O->transparency;
-    const int lb = O->leaf_begin, le = lb + O->leaf_count;
-    for (int l = lb; l < le && !zero; ++l) {
-      cptr<RtLeaf> L = &S.leaves[l];
-      if (O->leaf_cull) {
-        if (L->cull == RT_CULL_ALWAYS) continue;
-        if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
-      }
-      double t0 = 0.0, t1 = 0.0;
-      const int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1, SHARE ? &shr : nullptr);
-      const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && SHARE && L->filter_const && !isnan(cr.inv.x));
-      const bool h0 = n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))));
-      const bool h1 = n >= 2 && t1 > EPS && t1 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t1))));
-      if (h0 || h1) {
-        if (tobj == 0.0) zero = true;
-        else other = true;
-      }
-    }
-  }
-  if (coop_any<G>(zero)) return 0.0;                       // the product is +-0 (shadow_early_out)
-  if (!coop_any<G>(other)) return 1.0;                     // no factor (transparency-1 objects skipped)
-  double t = 1.0;                                          // factors other than 0: the exact product
-  if (gsub == 0) t = shadow_transparency<SHARE, false, false>(S, p, dir, dist);
-  return __shfl(t, (int)(__lane_id() & ~(unsigned)(G - 1)));
-}
-
 // One ray of trace()'s loop body: nearest hit, the light loop (shadow rays first, then the shading
 // inputs), the inside test and the refraction / reflection decisions (raytracer.rs:141-280).
-// G > 1: cooperative ray groups (nearest_hit_coop / shadow_transparency_coop); every lane of a group
-// holds the same ray and computes the same values from the group's reductions.
-template <bool REFR, bool FC, int G = 1>
+template <bool REFR, bool FC>
 __device__ __forceinline__ void wf_ray(const DS& S, V3 ro, V3 rd, int depth, int max_depth, Col* Lo, double* wt,
-                                       double* wr, bool* ch_t, bool* ch_r, V3* po, V3* dt, V3* dr, int gsub = 0) {
+                                       double* wr, bool* ch_t, bool* ch_r, V3* po, V3* dt, V3* dr) {
   constexpr bool SHARE = REFR && RT_SPHERE_SHARE, OBB = !REFR;
   *ch_t = *ch_r = false;
   *Lo = {0.0, 0.0, 0.0};
   *wt = *wr = 0.0;
   double t_hit;
-  int oi;
-  if constexpr (G > 1) oi = nearest_hit_coop<SHARE, G>(S, ro, rd, gsub, &t_hit);
-  else oi = nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit, depth == 0 ? 0 : 1);
+  const int oi = nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit, depth == 0 ? 0 : 1);
   if (oi < 0) return;                                                   // Color::BLACK (:152-160)
   const V3 p = add(ro, scale(rd, t_hit));                               // :162
   V3 nrm = {0.0, 0.0, 0.0};
@@ -1582,10 +1472,7 @@ __device__ __forceinline__ void wf_ray(const DS& S, V3 ro, V3 rd, int depth, int
     double ll, ill;
     len_inv(lv, &ll, &ill);
     const V3 sdir = scale(lv, ill);
-    double t;
-    if constexpr (G > 1) t = S.shadow_early_out ? shadow_transparency_coop<SHARE, G>(S, p, sdir, ll, gsub)
-                                                : shadow_transparency<SHARE, OBB>(S, p, sdir, ll);
-    else t = shadow_transparency<SHARE, OBB>(S, p, sdir, ll);
+    const double t = shadow_transparency<SHARE, OBB>(S, p, sdir, ll);
     if (!have_shading) {
       shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
       L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));
@@ -1628,16 +1515,13 @@ __device__ __forceinline__ void wf_ray(const DS& S, V3 ro, V3 rd, int depth, int
 #ifndef RT_WAVES_PER_EU_WF
 #define RT_WAVES_PER_EU_WF 5
 #endif
-#ifndef RT_WF_GROUP_DEFAULT
-#define RT_WF_GROUP_DEFAULT 8          // lanes per ray on the wavefront path's levels >= 1
-#endif
-// One workgroup (wave) per 64 / G rays of level d (n of them): level 0 = the pixel slots in tile
-// order, levels >= 1 in key order (A.perm); G lanes per ray (cooperative ray groups, G > 1).
-template <bool REFR, bool FC, int G = 1>
+// One workgroup (wave) per 64 rays of level d (n of them): level 0 = the pixel slots in tile order,
+// levels >= 1 in key order (A.perm).
+template <bool REFR, bool FC>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_WF))) void wf_trace_kernel(
     RtDevScene S, WfArena A, int d, uint32_t n, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth) {
-  const int lane = threadIdx.x & 63, gsub = lane % G;
-  const uint32_t i = blockIdx.x * (64u / G) + (uint32_t)(lane / G);
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
   bool live = i < n;
   const WfLevel lv = wf_level(A, d);
   V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
@@ -1657,11 +1541,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER
   double wt = 0.0, wr = 0.0;
   bool ch_t = false, ch_r = false;
   V3 p = {0.0, 0.0, 0.0}, dt = {0.0, 0.0, 0.0}, dr = {0.0, 0.0, 0.0};
-  if (live) wf_ray<REFR, FC, G>(make_ds(S), ro, rd, d, max_depth, &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr, gsub);
-  if (gsub != 0) {                                            // a group's first lane speaks for its ray
-    live = false;
-    ch_t = ch_r = false;
-  }
+  if (live) wf_ray<REFR, FC>(make_ds(S), ro, rd, d, max_depth, &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr);
   int32_t ct = -1, cr = -1;
   const uint64_t bt = __ballot(ch_t), br = __ballot(ch_r);
   const uint32_t nt = (uint32_t)__popcll(bt), nr = (uint32_t)__popcll(br);
@@ -2115,7 +1995,6 @@ struct rt_ctx {
   bool tile_order = true;               // rt_ctx_set_option(RT_OPT_TILE_ORDER): cost-ordered dispatch
   bool fast_clamp = true;               // rt_ctx_set_option(RT_OPT_FAST_CLAMP): min/max clamps where exact
   int wf_cap_pct = 200;                 // rt_ctx_set_option(RT_OPT_WAVEFRONT_CAP): rays per level, % of pixel slots
-  int wf_group = RT_WF_GROUP_DEFAULT;   // rt_ctx_set_option(RT_OPT_WAVEFRONT_GROUP): lanes per ray on levels >= 1
   double wf_klo[3] = {-100, -100, -100}, wf_khi[3] = {100, 100, 100};   // coherence-key extent (bounded objects)
   int n_cu = 256;                       // compute units of the device (wave slots = n_cu x 4 SIMDs x waves/SIMD)
   bool uploaded = false;
@@ -2395,17 +2274,11 @@ static int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, i
       RT_HIP(rt_wf_sort_pairs(tmp, &tb, L.key, kout, L.val, perm, (int)n, 30, st));
       A.perm = perm;
     }
-    const int G = d == 0 ? 1 : c->wf_group;
-    const dim3 g((n + 64 / G - 1) / (64 / G));
-#define RT_WF_TRACE(Gv)                                                                                                 \
-    if (refr && fc) hipLaunchKernelGGL((wf_trace_kernel<true, true, Gv>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth); \
-    else if (refr) hipLaunchKernelGGL((wf_trace_kernel<true, false, Gv>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth); \
-    else if (fc) hipLaunchKernelGGL((wf_trace_kernel<false, true, Gv>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth); \
-    else hipLaunchKernelGGL((wf_trace_kernel<false, false, Gv>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
-    if (G == 8) { RT_WF_TRACE(8) }
-    else if (G == 4) { RT_WF_TRACE(4) }
-    else { RT_WF_TRACE(1) }
-#undef RT_WF_TRACE
+    const dim3 g((n + 63) / 64);
+    if (refr && fc) hipLaunchKernelGGL((wf_trace_kernel<true, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    else if (refr) hipLaunchKernelGGL((wf_trace_kernel<true, false>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    else if (fc) hipLaunchKernelGGL((wf_trace_kernel<false, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    else hipLaunchKernelGGL((wf_trace_kernel<false, false>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
     RT_HIP(hipGetLastError());
     if (d < max_depth) {
       uint32_t cnt = 0;
@@ -2979,11 +2852,6 @@ int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
     if (value != 0 && value != 1) return fail(RT_ERR_INVALID, "RT_OPT_TIMING value %d", value);
     c->timing = value != 0;
     c->timed = false;                  // no launch recorded under the new setting yet
-    return RT_OK;
-  }
-  if (option == RT_OPT_WAVEFRONT_GROUP) {
-    if (value != 1 && value != 4 && value != 8) return fail(RT_ERR_INVALID, "RT_OPT_WAVEFRONT_GROUP %d not 1, 4 or 8", value);
-    c->wf_group = value;
     return RT_OK;
   }
   if (option == RT_OPT_WAVEFRONT_CAP) {

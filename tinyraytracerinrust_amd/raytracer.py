@@ -302,11 +302,6 @@ class Renderer:
         percent of the launch's pixel slots (pixels whose tree overflows are re-rendered, same bits)."""
         check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_WAVEFRONT_CAP, int(percent)))
 
-    def set_wavefront_group(self, lanes: int) -> None:
-        """rt_ctx_set_option(RT_OPT_WAVEFRONT_GROUP): lanes per ray (1, 4 or 8) on the wavefront path's
-        levels >= 1; a ray's lanes split the scene's objects (same pixels)."""
-        check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_WAVEFRONT_GROUP, int(lanes)))
-
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()
         check(lib().rt_ctx_last_kernel_ms(self.h, ctypes.byref(ms)))

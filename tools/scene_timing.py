@@ -24,10 +24,7 @@ for d in depths:
         rt.max_depth = d
         rt.load_scene(text, t, asset_dir=S)
         r = rt.renderer
-        kern, _, opt = k.partition(":")           # e.g. wavefront:g8 (RT_OPT_WAVEFRONT_GROUP)
-        r.set_kernel(kern)
-        if opt.startswith("g"):
-            r.set_wavefront_group(int(opt[1:]))
+        r.set_kernel(k)
         out = r.render_rows(0, H)
         torch.cuda.synchronize()
         cal = r.last_kernel_ms()
