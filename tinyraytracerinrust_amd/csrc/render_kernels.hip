@@ -172,6 +172,9 @@ constexpr double EPS = RT_EPSILON;
 #ifndef RT_SPHERE_SHARE
 #define RT_SPHERE_SHARE 1           // concentric sphere leaves with one transform share their ray terms
 #endif
+#ifndef RT_SPHERE_SHARE_CHAIN
+#define RT_SPHERE_SHARE_CHAIN 1     // the refraction-chain kernel shares sphere terms too
+#endif
 constexpr double PI_D = 3.14159265358979323846;   // std::f64::consts::PI
 
 struct V3 { double x, y, z; };
@@ -880,7 +883,7 @@ __device__ Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullpt
   // the registers (104 -> 116 VGPRs, no spill; spinning_globes 1080p 4.8 % faster), while the
   // reflection-only megakernel at 5 waves spills 14 more VGPRs and runs 6 % slower on 4K globes
   // (profiles/r02am_ab.txt).
-  constexpr bool SHARE = REFR && RT_SPHERE_SHARE;
+  constexpr bool SHARE = REFR && RT_SPHERE_SHARE && (!CHAIN || RT_SPHERE_SHARE_CHAIN);
   constexpr bool OBB = !REFR;                          // oriented object boxes: reflection-only kernels
   int fSlot[RECORD ? RT_MAX_DEPTH_CAP : 1];
   [[maybe_unused]] int ray_type = 0, slot = 0;                  // RayType::NormalRay
