@@ -250,9 +250,14 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  * compare/select form everywhere (A/B checks).
  * RT_OPT_WAVEFRONT_CAP: rays each recursion level of the wavefront path holds, in percent of the
  * launch's pixel slots (1..400, default 200); a pixel whose ray tree overflows a level is rendered
- * again by the per-lane megakernel (same bits), so the value trades memory against that fallback. */
+ * again by the per-lane megakernel (same bits), so the value trades memory against that fallback.
+ * RT_OPT_WAVEFRONT_PAIRS: how the wavefront path traces a level's rays: 0 one wave walks the object
+ * hierarchy for 64 rays (wf_trace_kernel); 1 (default) levels >= 1 go through (ray, object) pairs
+ * sorted by object, so a wave tests one object against 64 rays (wfp_* kernels; scenes whose shadow
+ * products are order-free, RtDevScene::shadow_pow, else as 0); 2 level 0 (the camera rays) too. */
 typedef enum rt_option {
-  RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4
+  RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4,
+  RT_OPT_WAVEFRONT_PAIRS = 5
 } rt_option;
 typedef enum rt_kernel_choice {
   RT_KERNEL_AUTO = 0, RT_KERNEL_MEGA = 1, RT_KERNEL_DEFERRED = 2, RT_KERNEL_WAVEFRONT = 3

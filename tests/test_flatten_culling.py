@@ -111,3 +111,18 @@ def test_ray_chain_flag():
     # -0 counts as zero, NaN as nonzero (IEEE comparisons, as the kernels test them)
     assert _flags(_dump("draw(sphere(<0, 0, 0>, 30, red, 0 * (0 - 1), 0.5))"))["ray_chains"] == 1
     assert _flags(_dump("draw(sphere(<0, 0, 0>, 30, red, 0.1, 0.5))"))["ray_chains"] == 0
+
+
+def test_shadow_pow_flag():
+    """shadow_pow (scene.cpp flatten): every transparency outside {+-0, 1} is one finite value, so a
+    shadow ray's product (raytracer.rs:181-197) is 0 or T^count whatever the order its hits are
+    found in -- the wavefront pair path's condition."""
+    def pw(text, t=0.0):
+        m = re.search(r"shadow_pow=(\d)", _dump(text, t))
+        assert m
+        return int(m.group(1))
+    assert pw(open(os.path.join(SCENES, "fractal.scene")).read()) == 1           # glass 0.6, the rest 0
+    assert pw(open(os.path.join(SCENES, "globes.scene")).read()) == 1            # all opaque
+    assert pw(open(os.path.join(SCENES, "spinning_globes.scene")).read(), 0.3) == 1
+    assert pw("draw(sphere(<0, 0, 0>, 30, red, 0, 0.5))\ndraw(sphere(<0, 9, 0>, 3, red, 0, 1))") == 1
+    assert pw("draw(sphere(<0, 0, 0>, 30, red, 0, 0.5))\ndraw(sphere(<0, 9, 0>, 3, red, 0, 0.25))") == 0

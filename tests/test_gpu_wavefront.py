@@ -19,7 +19,7 @@ CASES = [("globes", 0.0, 160, 120, 10), ("globes", 0.25, 640, 480, 10), ("globes
          ("spinning_gimbals", 0.4, 160, 120, 10), ("fractal", 0.0, 160, 120, 10), ("fractal", 0.0, 96, 72, 2)]
 
 
-def _render(text, t, W, H, d, cap=None, rows=None):
+def _render(text, t, W, H, d, cap=None, rows=None, pairs=None):
     import tinyraytracerinrust_amd as T
     rt = T.RayTracer(W, H)
     rt.max_depth = d
@@ -28,24 +28,48 @@ def _render(text, t, W, H, d, cap=None, rows=None):
     r.set_kernel("wavefront")
     if cap is not None:
         r.set_wavefront_cap(cap)
+    if pairs is not None:
+        r.set_wavefront_pairs(pairs)
     y0, y1 = rows or (0, H)
     return r.render_rows_host(y0, y1), r.render_rows_host(y0, y1, f64=True)
 
 
+@pytest.mark.parametrize("pairs", [0, 1, 2])
 @pytest.mark.parametrize("name,t,W,H,d", CASES)
-def test_wavefront_parity(worldmap, name, t, W, H, d):
+def test_wavefront_parity(worldmap, name, t, W, H, d, pairs):
+    """RT_OPT_WAVEFRONT_PAIRS 0: every level's rays walk the hierarchy a wave at a time; 1: levels >= 1
+    go through (ray, object) pairs sorted by object (the wfp_* kernels); 2: level 0 too."""
     from oracle import oracle as O
-    gu, gf = _render(scene_text(name), t, W, H, d)
+    gu, gf = _render(scene_text(name), t, W, H, d, pairs=pairs)
     rf, ru = O.OracleScene(scene_text(name), t, W, H, max_depth=d).render(0, H, f64=True)
-    assert_close(gu, gf, ru, rf, f"wavefront {name} t={t} {W}x{H} d={d}")
+    assert_close(gu, gf, ru, rf, f"wavefront {name} t={t} {W}x{H} d={d} pairs={pairs}")
 
 
+def test_wavefront_pairs_one_object_many_hits(worldmap):
+    """Shadow rays through several glass shells of one transparency (the pair path folds a count: T^k)
+    and rays that meet coincident surfaces (the nearest-hit tie goes to the first object drawn)."""
+    from oracle import oracle as O
+    text = ("draw(sphere(<0, 0, 0>, 30, rgb(0.9, 0.9, 0.9), 0, 0.7))\n"
+            "draw(sphere(<0, 0, 0>, 20, rgb(0.9, 0.5, 0.5), 0, 0.7))\n"
+            "draw(sphere(<0, 0, 0>, 10, rgb(0.5, 0.9, 0.5), 0.3, 0.7))\n"
+            "draw(sphere(<25, 0, 0>, 10, rgb(0.5, 0.5, 0.9), 0.5))\n"
+            "draw(sphere(<25, 0, 0>, 10, rgb(0.9, 0.9, 0.1), 0.5))\n"
+            "draw(plane(<0, 1, 0>, 40, blue, 0.3))\n"
+            "append light(<0, 80, -60>, rgb(0.6, 0.6, 0.6), 100)\n")
+    W, H, d = 160, 120, 10
+    for pairs in (0, 1, 2):
+        gu, gf = _render(text, 0.0, W, H, d, pairs=pairs)
+        rf, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H, f64=True)
+        assert_close(gu, gf, ru, rf, f"wavefront shells pairs={pairs}")
+
+
+@pytest.mark.parametrize("pairs", [0, 2])
 @pytest.mark.parametrize("name,t", [("fractal", 0.0), ("spinning_globes", 0.3), ("globes", 0.0)])
-def test_wavefront_level_overflow_fixup(worldmap, name, t):
+def test_wavefront_level_overflow_fixup(worldmap, name, t, pairs):
     """Levels of 1 % of the pixel slots: most trees overflow, and their pixels come from the fix-up."""
     from oracle import oracle as O
     W, H, d = 128, 96, 10
-    gu, gf = _render(scene_text(name), t, W, H, d, cap=1)
+    gu, gf = _render(scene_text(name), t, W, H, d, cap=1, pairs=pairs)
     rf, ru = O.OracleScene(scene_text(name), t, W, H, max_depth=d).render(0, H, f64=True)
     assert_close(gu, gf, ru, rf, f"wavefront overflow {name}")
 
@@ -76,14 +100,15 @@ def test_wavefront_rows_and_bands(worldmap):
     assert np.array_equal(frame.cpu().numpy(), ref_u8)
 
 
+@pytest.mark.parametrize("pairs", [0, 2])
 @pytest.mark.parametrize("seed", range(5000, 5032))
-def test_wavefront_random_scenes(seed):
+def test_wavefront_random_scenes(seed, pairs):
     """Seeded random scenes (trees and chains, odd materials) through the wavefront path."""
     from tests.scene_fuzz import random_scene
     from oracle import oracle as O
     text = random_scene(seed, chains=seed % 2 == 1)
     W, H, d = 96, 72, 6
-    gu, gf = _render(text, 0.0, W, H, d)
+    gu, gf = _render(text, 0.0, W, H, d, pairs=pairs)
     rf, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H, f64=True)
     assert_close(gu, gf, ru, rf, f"wavefront random scene {seed}")
 
@@ -95,6 +120,9 @@ def test_wavefront_option_bounds():
     for bad in (0, 401):
         with pytest.raises(T.RtError):
             rt.renderer.set_wavefront_cap(bad)
+    for bad in (-1, 3, 8):
+        with pytest.raises(T.RtError):
+            rt.renderer.set_wavefront_pairs(bad)
 
 
 @pytest.mark.parametrize("name,t", [("fractal", 0.0), ("fractal", 0.5)])

@@ -823,9 +823,10 @@ typedef LDS_AS double lds_f64;
 #ifndef RT_LDS_FRAMES
 #define RT_LDS_FRAMES 2
 #endif
-// Refraction-chain kernels (RT_MODE_CHAIN): frames of the chain stack kept in LDS.
+// Refraction-chain kernels (RT_MODE_CHAIN): frames of the chain stack kept in LDS.  At 4 waves/SIMD
+// (below) 5 frames fill the 160 KB of a CU (10 KB per one-wave workgroup).
 #ifndef RT_LDS_FRAMES_CHAIN
-#define RT_LDS_FRAMES_CHAIN RT_LDS_FRAMES
+#define RT_LDS_FRAMES_CHAIN 5
 #endif
 // Refraction frames also carry the pending reflection ray (P, D, rp: 7 doubles); the first
 // KLR of them go to LDS after the KL colour frames, [frame][component][lane] likewise.
@@ -1245,8 +1246,13 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
 #ifndef RT_WAVES_PER_EU_NOREFR
 #define RT_WAVES_PER_EU_NOREFR 5
 #endif
+// The chain kernel at 4 waves/SIMD keeps every VGPR in registers (115) and 5 stack frames in LDS:
+// anim120 moves 48.8 MB of HBM per 1080p frame (27 MB written, 3.3x the frame) at 9 201 Mrays/s.
+// At 5 waves/SIMD it spills 27 VGPRs inside the traversal loops and moves 481.7 MB per frame (317 MB
+// written) for 9 680 Mrays/s (+5 %); 5 waves without the shared sphere terms (14 spills) 216 MB at
+// 8 814 (profiles/r03k_anim_variants.txt).  The traffic budget wins over 5 %, as for the megakernel.
 #ifndef RT_WAVES_PER_EU_CHAIN
-#define RT_WAVES_PER_EU_CHAIN 5
+#define RT_WAVES_PER_EU_CHAIN 4
 #endif
 #define RT_WAVES(REFR) ((REFR) ? RT_WAVES_PER_EU : RT_WAVES_PER_EU_NOREFR)
 #define RT_WAVES_MODE(M) ((M) == RT_MODE_REFL ? RT_WAVES_PER_EU_NOREFR : (M) == RT_MODE_CHAIN ? RT_WAVES_PER_EU_CHAIN : RT_WAVES_PER_EU)
@@ -1453,15 +1459,17 @@ __device__ __forceinline__ uint32_t wf_key(const WfArena& A, V3 o, V3 d) {
 
 // One ray of trace()'s loop body: nearest hit, the light loop (shadow rays first, then the shading
 // inputs), the inside test and the refraction / reflection decisions (raytracer.rs:141-280).
-template <bool REFR, bool FC>
-__device__ __forceinline__ void wf_ray(const DS& S, V3 ro, V3 rd, int depth, int max_depth, Col* Lo, double* wt,
-                                       double* wr, bool* ch_t, bool* ch_r, V3* po, V3* dt, V3* dr) {
-  constexpr bool SHARE = REFR && RT_SPHERE_SHARE, OBB = !REFR;
+// NH(&t) gives the nearest hit (object, distance), SH(k, p, sdir, dist) light k's shadow
+// transparency: the traversals themselves (wf_ray) or the pair path's folded results (wfp_shade).
+template <bool REFR, bool FC, class NH, class SH>
+__device__ __forceinline__ void wf_ray_core(const DS& S, V3 ro, V3 rd, int depth, int max_depth, NH&& nh, SH&& sh,
+                                            Col* Lo, double* wt, double* wr, bool* ch_t, bool* ch_r, V3* po, V3* dt,
+                                            V3* dr) {
   *ch_t = *ch_r = false;
   *Lo = {0.0, 0.0, 0.0};
   *wt = *wr = 0.0;
   double t_hit;
-  const int oi = nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit, depth == 0 ? 0 : 1);
+  const int oi = nh(&t_hit);
   if (oi < 0) return;                                                   // Color::BLACK (:152-160)
   const V3 p = add(ro, scale(rd, t_hit));                               // :162
   V3 nrm = {0.0, 0.0, 0.0};
@@ -1475,7 +1483,7 @@ __device__ __forceinline__ void wf_ray(const DS& S, V3 ro, V3 rd, int depth, int
     double ll, ill;
     len_inv(lv, &ll, &ill);
     const V3 sdir = scale(lv, ill);
-    const double t = shadow_transparency<SHARE, OBB>(S, p, sdir, ll);
+    const double t = sh(k, p, sdir, ll);
     if (!have_shading) {
       shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
       L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));
@@ -1515,36 +1523,22 @@ __device__ __forceinline__ void wf_ray(const DS& S, V3 ro, V3 rd, int depth, int
   if (do_refl) *dr = reflect_dir(rd, n2);
 }
 
-#ifndef RT_WAVES_PER_EU_WF
-#define RT_WAVES_PER_EU_WF 5
-#endif
-// One workgroup (wave) per 64 rays of level d (n of them): level 0 = the pixel slots in tile order,
-// levels >= 1 in key order (A.perm).
 template <bool REFR, bool FC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_WF))) void wf_trace_kernel(
-    RtDevScene S, WfArena A, int d, uint32_t n, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
-  bool live = i < n;
-  const WfLevel lv = wf_level(A, d);
-  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
-  uint32_t j = i;                                            // the ray's slot in its level
-  int32_t pix = (int32_t)i;
-  if (d == 0) {
-    int x, r, y;
-    live = live && wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y);
-    if (live) camera_ray(S.cam, (double)x, (double)y, &ro, &rd);          // get_pixel(x as f64, y as f64)
-  } else if (live) {
-    j = A.perm ? A.perm[i] : i;
-    ro = {lv.ox[j], lv.oy[j], lv.oz[j]};
-    rd = {lv.dx[j], lv.dy[j], lv.dz[j]};
-    pix = lv.pix[j];
-  }
-  Col L = {0.0, 0.0, 0.0};
-  double wt = 0.0, wr = 0.0;
-  bool ch_t = false, ch_r = false;
-  V3 p = {0.0, 0.0, 0.0}, dt = {0.0, 0.0, 0.0}, dr = {0.0, 0.0, 0.0};
-  if (live) wf_ray<REFR, FC>(make_ds(S), ro, rd, d, max_depth, &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr);
+__device__ __forceinline__ void wf_ray(const DS& S, V3 ro, V3 rd, int depth, int max_depth, Col* Lo, double* wt,
+                                       double* wr, bool* ch_t, bool* ch_r, V3* po, V3* dt, V3* dr) {
+  constexpr bool SHARE = REFR && RT_SPHERE_SHARE, OBB = !REFR;
+  wf_ray_core<REFR, FC>(
+      S, ro, rd, depth, max_depth, [&](double* t) { return nearest_hit<SHARE, OBB>(S, ro, rd, t, depth == 0 ? 0 : 1); },
+      [&](int, V3 p, V3 sdir, double ll) { return shadow_transparency<SHARE, OBB>(S, p, sdir, ll); }, Lo, wt, wr, ch_t,
+      ch_r, po, dt, dr);
+}
+
+// The rays a wave's hits spawn, appended to level d + 1 (one ballot per kind, ONE atomic per
+// wave: the wave's refraction children, then its reflection children, in lane order), and the hit
+// record at the ray's slot j.
+__device__ __forceinline__ void wf_append(const WfArena& A, const WfLevel& lv, int d, int lane, bool live, uint32_t j,
+                                          int32_t pix, Col L, double wt, double wr, bool ch_t, bool ch_r, V3 p, V3 dt,
+                                          V3 dr) {
   int32_t ct = -1, cr = -1;
   const uint64_t bt = __ballot(ch_t), br = __ballot(ch_r);
   const uint32_t nt = (uint32_t)__popcll(bt), nr = (uint32_t)__popcll(br);
@@ -1579,6 +1573,39 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER
     lv.Lr[j] = L.r; lv.Lg[j] = L.g; lv.Lb[j] = L.b; lv.wt[j] = wt; lv.wr[j] = wr;
     lv.ct[j] = ct; lv.cr[j] = cr;
   }
+}
+
+#ifndef RT_WAVES_PER_EU_WF
+#define RT_WAVES_PER_EU_WF 5
+#endif
+// One workgroup (wave) per 64 rays of level d (n of them): level 0 = the pixel slots in tile order,
+// levels >= 1 in key order (A.perm).
+template <bool REFR, bool FC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_WF))) void wf_trace_kernel(
+    RtDevScene S, WfArena A, int d, uint32_t n, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+  bool live = i < n;
+  const WfLevel lv = wf_level(A, d);
+  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+  uint32_t j = i;                                            // the ray's slot in its level
+  int32_t pix = (int32_t)i;
+  if (d == 0) {
+    int x, r, y;
+    live = live && wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y);
+    if (live) camera_ray(S.cam, (double)x, (double)y, &ro, &rd);          // get_pixel(x as f64, y as f64)
+  } else if (live) {
+    j = A.perm ? A.perm[i] : i;
+    ro = {lv.ox[j], lv.oy[j], lv.oz[j]};
+    rd = {lv.dx[j], lv.dy[j], lv.dz[j]};
+    pix = lv.pix[j];
+  }
+  Col L = {0.0, 0.0, 0.0};
+  double wt = 0.0, wr = 0.0;
+  bool ch_t = false, ch_r = false;
+  V3 p = {0.0, 0.0, 0.0}, dt = {0.0, 0.0, 0.0}, dr = {0.0, 0.0, 0.0};
+  if (live) wf_ray<REFR, FC>(make_ds(S), ro, rd, d, max_depth, &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr);
+  wf_append(A, lv, d, lane, live, j, pix, L, wt, wr, ch_t, ch_r, p, dt, dr);
 }
 
 template <bool F64, bool FC>
@@ -1642,6 +1669,352 @@ __global__ __launch_bounds__(64) void wf_fixup_kernel(RtDevScene S, WfArena A, i
       ((uint32_t*)row)[x] = to_u8(C.r) | (to_u8(C.g) << 8) | (to_u8(C.b) << 16) | (255u << 24);
     }
   }
+}
+
+// ---------------------------------------------------------------- wavefront pair path
+// A level's rays are incoherent after a few bounces through scenes of many objects (fractal.scene:
+// 171 objects, glass spheres in hollow CSG cubes).  A wave that walks the hierarchy for 64 scattered
+// rays visits the union of their paths: on fractal.scene only 14 % / 22 % of the lanes are active in
+// a secondary / shadow leaf evaluation, and every level's pass takes as long as a wave's walk over
+// most of the scene (0.6-2 ms even for 25 000 rays).  The pair path splits the traversal into
+// (ray, object) work items and evaluates them object by object:
+//   wfp_cand_kernel<false>   per ray: the hierarchy walk with box tests only (no leaf), emitting a
+//                            pair (object, ray) for every object box the ray meets (through a per-wave
+//                            LDS buffer, one atomic per RT_WFP_BUF pairs);
+//   sort                     the pairs by object (rocPRIM radix sort), so a wave evaluates ONE object
+//                            (scalar loads of its leaves, every lane busy) for 64 different rays;
+//   wfp_near_eval_kernel     per pair: the object's nearest accepted distance (leaf tests, CSG filters:
+//                            nearest_hit's object body); atomicMin of its bits into the ray's best;
+//   wfp_near_tie_kernel      per pair at the ray's best distance: atomicMin of the object index.  The
+//                            nearest hit is the least (distance, object) -- exactly nearest_hit's
+//                            draw-order first-wins rule (raytracer.rs:141-150);
+//   wfp_cand_kernel<true>    per ray with a hit and per light: the shadow ray's candidate objects;
+//   sort, wfp_shadow_eval    per pair: the object's filtered hits with EPS < t < dist; a hit of a
+//                            zero-transparency object marks the shadow ray opaque, other hits add to
+//                            its count.  RtDevScene::shadow_pow (scene.cpp) guarantees the product in
+//                            draw order is then 0 or T^count, order-free (raytracer.rs:181-197);
+//   wfp_shade_kernel         per ray: wf_ray_core's shading, refraction and reflection decisions with
+//                            the folded results, then wf_append, as wf_trace_kernel.
+// Every value is computed by the same operations as the traversals; culling stays conservative
+// (the candidate walk tests boxes against the whole ray, tmax = infinity for the nearest hit).
+struct WfPairs {
+  uint32_t *key, *val;          // pairs as emitted: object, ray id (level slot, or slot * n_lights + light)
+  uint32_t *key_s, *val_s;      // sorted by object
+  double* tp;                   // nearest pass: the sorted pair's object's nearest accepted distance
+  uint32_t* count;              // pairs emitted (may exceed cap: the host grows the arena and re-runs)
+  uint32_t* bins;               // bucket-sort scratch (RT_BS_MAX_BINS words)
+  uint32_t cap;
+  unsigned long long* tmin;     // per ray of the level: nearest accepted distance (bits; +inf: none)
+  int32_t* omin;                // per ray: the least object index at that distance (INT_MAX: none)
+  double *px, *py, *pz;         // per ray: the hit point
+  uint32_t *kcnt, *opq;         // per shadow ray: hits of transparency-T objects / of a zero-transparency one
+  uint32_t *hkey, *hval, *hkey_s, *hperm;   // per ray: hit-point key, slot; sorted: the shadow / shading order
+};
+#ifndef RT_WFP_BUF
+#define RT_WFP_BUF 512          // pairs buffered in LDS per wave before one atomic allocates their slots
+#endif
+constexpr unsigned long long RT_WFP_NONE = 0x7FF0000000000000ull;   // +inf
+
+// Ray of slot j of level d (level 0: the pixel slot's camera ray).
+__device__ __forceinline__ bool wf_get_ray(const RtDevScene& S, const WfLevel& lv, int d, uint32_t j, int y_first,
+                                           int band_rows, int band_pitch, int n_rows, V3* ro, V3* rd) {
+  if (d == 0) {
+    int x, r, y;
+    if (!wf_pixel(S, j, y_first, band_rows, band_pitch, n_rows, &x, &r, &y)) return false;
+    camera_ray(S.cam, (double)x, (double)y, ro, rd);
+    return true;
+  }
+  *ro = {lv.ox[j], lv.oy[j], lv.oz[j]};
+  *rd = {lv.dx[j], lv.dy[j], lv.dz[j]};
+  return true;
+}
+
+// One wave per 64 rays of level d (in key order).  SHADOW = false: every object whose box the ray
+// meets; true: per light, every object whose box the shadow segment meets (objects of transparency 1
+// skipped, as shadow_transparency does).
+// Each lane walks its own path through the hierarchy (per-lane vector loads of one 64-byte RtTrav
+// record per step, which carries the object's box and flags): a wave-uniform walk visits the union
+// of its 64 rays' paths, measured 4-20 % slower here (profiles/r03m_pairs_fractal_timing.txt).
+template <bool SHADOW>
+__global__ __launch_bounds__(64) void wfp_cand_kernel(RtDevScene S, WfArena A, WfPairs P, int d, uint32_t n,
+                                                      int y_first, int band_rows, int band_pitch, int n_rows) {
+  __shared__ uint32_t sk[RT_WFP_BUF], sv[RT_WFP_BUF];
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+  const WfLevel lv = wf_level(A, d);
+  const DS D = make_ds(S);
+  bool live = i < n;
+  uint32_t j = i;
+  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+  if (live) {
+    j = SHADOW ? P.hperm[i] : (d > 0 && A.perm) ? A.perm[i] : i;
+    if (!SHADOW) live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
+  }
+  uint32_t nb = 0;                                           // wave-uniform fill of the LDS buffer
+  auto flush = [&]() {
+    __syncthreads();
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(P.count, nb);
+    base = (uint32_t)__shfl((int)base, 0);
+    for (uint32_t q = (uint32_t)lane; q < nb; q += 64)
+      if (base + q < P.cap) { P.key[base + q] = sk[q]; P.val[base + q] = sv[q]; }
+    __syncthreads();
+    nb = 0;
+  };
+  auto emit = [&](bool h, uint32_t ob, uint32_t id) {
+    const uint64_t m = __ballot(h);
+    if (!m) return;
+    const uint32_t c = (uint32_t)__popcll(m);
+    if (nb + c > RT_WFP_BUF) flush();
+    if (h) {
+      const uint32_t q = nb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      sk[q] = ob;
+      sv[q] = id;
+    }
+    nb += c;
+  };
+  auto walk = [&](bool act0, V3 o, V3 dir, double tmax, uint32_t id) {
+    const CullRay cr = cull_ray(o, dir);
+    const RtTrav* __restrict__ TR = S.trav;
+    const int nt = S.n_trav;
+    int t = act0 ? 0 : nt;
+    while (__ballot(t < nt)) {
+      bool h = false;
+      int ob = 0;
+      if (t < nt) {
+        const RtTrav T = TR[t];
+        const bool in = box_may_hit(T.blo, T.bhi, cr, tmax);
+        if (T.obj < 0) {
+          t = in ? t + 1 : T.skip;
+        } else {
+          ++t;
+          ob = T.obj;
+          h = T.cull != RT_CULL_ALWAYS && !(SHADOW && T.shadow_skip) && (T.cull != RT_CULL_BOX || in);
+        }
+      }
+      emit(h, (uint32_t)ob, id);
+    }
+  };
+  if constexpr (!SHADOW) {
+    if (i < n) { P.tmin[j] = RT_WFP_NONE; P.omin[j] = 0x7fffffff; }   // slots outside the frame too
+    walk(live, ro, rd, INFINITY, j);
+  } else {
+    const int32_t oi = live ? P.omin[j] : 0x7fffffff;
+    const bool hit = live && oi != 0x7fffffff;
+    V3 p = {0.0, 0.0, 0.0};
+    if (hit) p = {P.px[j], P.py[j], P.pz[j]};                     // wfp_hit_key_kernel
+    for (int k = 0; k < D.n_lights; ++k) {
+      V3 sdir = {0.0, 0.0, 0.0};
+      double tmax = 0.0;
+      const uint32_t s = j * (uint32_t)D.n_lights + (uint32_t)k;
+      if (hit) {
+        cptr<RtLight> lt = &D.lights[k];
+        const V3 l = sub(ld3(lt->p), p);
+        double ll, ill;
+        len_inv(l, &ll, &ill);
+        sdir = scale(l, ill);
+        tmax = cull_tmax(ll);
+        P.kcnt[s] = 0;
+        P.opq[s] = 0;
+      }
+      walk(hit, p, sdir, tmax, s);
+    }
+  }
+  flush();
+}
+
+// The object's nearest accepted distance for one ray: nearest_hit's body for one object, its best
+// starting at +inf (the leaf boxes' tmax only shrinks, as share_prev requires).
+__device__ __forceinline__ double wfp_object_nearest(const DS& S, int o, V3 ro, V3 rd, const CullRay& cr) {
+  cptr<RtObject> O = &S.objects[o];
+  const bool fin = wave_finite(ro, rd);
+  double best = INFINITY;
+  SphereShare shr = {0.0, 0.0, 0.0};
+  const int lb = O->leaf_begin, le = lb + O->leaf_count;
+  for (int l = lb; l < le; ++l) {
+    cptr<RtLeaf> L = &S.leaves[l];
+    if (O->leaf_cull) {
+      if (L->cull == RT_CULL_ALWAYS) continue;
+      if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, cull_tmax(best))) continue;
+    }
+    double t0 = 0.0, t1 = 0.0;
+    const int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1, RT_SPHERE_SHARE ? &shr : nullptr);
+    const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && L->filter_const && !isnan(cr.inv.x));
+    if (n >= 1 && t0 > EPS && t0 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) best = t0;
+    if (n >= 2 && t1 > EPS && t1 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t1))))) best = t1;
+  }
+  return best;
+}
+
+// Filtered hits of the object with EPS < t < dist on one shadow ray (shadow_transparency's body for
+// one object); a zero-transparency object stops at its first.
+__device__ __forceinline__ uint32_t wfp_object_shadow(const DS& S, int o, V3 p, V3 dir, double dist, const CullRay& cr) {
+  cptr<RtObject> O = &S.objects[o];
+  const bool fin = wave_finite(p, dir);
+  const double tmax = cull_tmax(dist);
+  const bool zero = O->transparency == 0.0;
+  uint32_t cnt = 0;
+  SphereShare shr = {0.0, 0.0, 0.0};
+  const int lb = O->leaf_begin, le = lb + O->leaf_count;
+  for (int l = lb; l < le; ++l) {
+    cptr<RtLeaf> L = &S.leaves[l];
+    if (O->leaf_cull) {
+      if (L->cull == RT_CULL_ALWAYS) continue;
+      if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
+    }
+    double t0 = 0.0, t1 = 0.0;
+    const int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1, RT_SPHERE_SHARE ? &shr : nullptr);
+    const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && L->filter_const && !isnan(cr.inv.x));
+    if (n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) {
+      ++cnt;
+      if (zero) return cnt;
+    }
+    if (n >= 2 && t1 > EPS && t1 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t1))))) {
+      ++cnt;
+      if (zero) return cnt;
+    }
+  }
+  return cnt;
+}
+
+// One lane per sorted pair: the waves see one object (two at a run boundary): scalarised over the
+// distinct objects of the wave as shade_inputs does, so every scene read is a scalar load.
+__global__ __launch_bounds__(64) void wfp_near_eval_kernel(RtDevScene S, WfArena A, WfPairs P, int d, uint32_t np,
+                                                           int y_first, int band_rows, int band_pitch, int n_rows) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+  const WfLevel lv = wf_level(A, d);
+  const DS D = make_ds(S);
+  bool live = i < np;
+  uint32_t o = 0xffffffffu, j = 0;
+  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+  if (live) {
+    o = P.key_s[i];
+    j = P.val_s[i];
+    live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
+  }
+  const CullRay cr = cull_ray(ro, rd);
+  double best = INFINITY;
+  uint64_t todo = __ballot(live);
+  while (todo) {
+    const uint32_t ou = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)__builtin_ctzll(todo));
+    const uint64_t mine = __ballot(live && o == ou);
+    todo &= ~mine;
+    if ((mine >> lane) & 1) best = wfp_object_nearest(D, (int)ou, ro, rd, cr);
+  }
+  if (live) {
+    P.tp[i] = best;
+    if (best < INFINITY) atomicMin(&P.tmin[j], (unsigned long long)__double_as_longlong(best));
+  }
+}
+
+__global__ __launch_bounds__(256) void wfp_near_tie_kernel(WfPairs P, uint32_t np) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
+    const double t = P.tp[i];
+    if (!(t < INFINITY)) continue;
+    const uint32_t j = P.val_s[i];
+    if ((unsigned long long)__double_as_longlong(t) == P.tmin[j]) atomicMin(&P.omin[j], (int32_t)P.key_s[i]);
+  }
+}
+
+// Per ray of the level, after the nearest-hit folds: the hit point (wf_ray_core's p) and a coherence
+// key for the shadow and shading passes, the Morton code of the hit point's cell (the light
+// directions from nearby points are alike, and nearby points mostly lie on the same object); misses
+// sort last.
+__global__ __launch_bounds__(256) void wfp_hit_key_kernel(RtDevScene S, WfArena A, WfPairs P, int d, uint32_t n,
+                                                          int y_first, int band_rows, int band_pitch, int n_rows) {
+  const WfLevel lv = wf_level(A, d);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t j = (d > 0 && A.perm) ? A.perm[i] : i;
+    V3 ro, rd;
+    uint32_t key = 0xffffffffu;
+    if (wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd) && P.omin[j] != 0x7fffffff) {
+      const V3 p = add(ro, scale(rd, __longlong_as_double((long long)P.tmin[j])));
+      P.px[j] = p.x; P.py[j] = p.y; P.pz[j] = p.z;
+      key = wf_key(A, p, V3{0.0, 0.0, 0.0}) & 0x07ffffffu;
+    }
+    P.hkey[i] = key;
+    P.hval[i] = j;
+  }
+}
+
+__global__ __launch_bounds__(64) void wfp_shadow_eval_kernel(RtDevScene S, WfPairs P, uint32_t np) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+  const DS D = make_ds(S);
+  const bool live = i < np;
+  uint32_t o = 0xffffffffu, s = 0;
+  V3 p = {0.0, 0.0, 0.0}, sdir = {0.0, 0.0, 0.0};
+  double ll = 0.0;
+  if (live) {
+    o = P.key_s[i];
+    s = P.val_s[i];
+    const uint32_t j = s / (uint32_t)S.n_lights, k = s % (uint32_t)S.n_lights;
+    p = {P.px[j], P.py[j], P.pz[j]};
+    const RtLight& lt = S.lights[k];
+    const V3 l = sub(V3{lt.p[0], lt.p[1], lt.p[2]}, p);              // wf_ray_core's light loop
+    double ill;
+    len_inv(l, &ll, &ill);
+    sdir = scale(l, ill);
+  }
+  const CullRay cr = cull_ray(p, sdir);
+  uint32_t cnt = 0;
+  uint64_t todo = __ballot(live);
+  while (todo) {
+    const uint32_t ou = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)__builtin_ctzll(todo));
+    const uint64_t mine = __ballot(live && o == ou);
+    todo &= ~mine;
+    if ((mine >> lane) & 1) cnt = wfp_object_shadow(D, (int)ou, p, sdir, ll, cr);
+  }
+  if (live && cnt) {
+    if (D.objects[o].transparency == 0.0) atomicOr(&P.opq[s], 1u);
+    else atomicAdd(&P.kcnt[s], cnt);
+  }
+}
+
+template <bool REFR, bool FC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_WF))) void wfp_shade_kernel(
+    RtDevScene S, WfArena A, WfPairs P, int d, uint32_t n, int y_first, int band_rows, int band_pitch, int n_rows,
+    int max_depth) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+  const WfLevel lv = wf_level(A, d);
+  bool live = i < n;
+  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+  uint32_t j = i;
+  int32_t pix = (int32_t)i;
+  if (live) {
+    j = P.hperm[i];                                          // hit-point order (wfp_hit_key_kernel)
+    live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
+    pix = d > 0 ? lv.pix[j] : (int32_t)j;
+  }
+  Col L = {0.0, 0.0, 0.0};
+  double wt = 0.0, wr = 0.0;
+  bool ch_t = false, ch_r = false;
+  V3 p = {0.0, 0.0, 0.0}, dt = {0.0, 0.0, 0.0}, dr = {0.0, 0.0, 0.0};
+  const uint32_t nl = (uint32_t)S.n_lights;
+  const double T = S.shadow_t;
+  if (live)
+    wf_ray_core<REFR, FC>(
+        make_ds(S), ro, rd, d, max_depth,
+        [&](double* t) {
+          const int32_t oi = P.omin[j];
+          if (oi == 0x7fffffff) { *t = INFINITY; return -1; }
+          *t = __longlong_as_double((long long)P.tmin[j]);
+          return (int)oi;
+        },
+        [&](int k, V3, V3, double) {
+          const uint32_t s = j * nl + (uint32_t)k;
+          if (P.opq[s]) return 0.0;
+          double tr = 1.0;                                     // shadow_transparency's product, order-free
+          for (uint32_t c = P.kcnt[s]; c > 0; --c) {
+            tr *= T;
+            if (tr == 0.0) return 0.0;
+          }
+          return tr;
+        },
+        &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr);
+  wf_append(A, lv, d, lane, live, j, pix, L, wt, wr, ch_t, ch_r, p, dt, dr);
 }
 
 template <bool REFR>
@@ -2008,6 +2381,12 @@ struct rt_ctx {
   size_t scratch_bytes = 0;
   void* wf = nullptr;                   // wavefront arena (levels, counters, overflow flags), grow-only
   size_t wf_bytes = 0;
+  int wf_pairs = 1;                     // rt_ctx_set_option(RT_OPT_WAVEFRONT_PAIRS): 0 off, 1 levels >= 1, 2 every level
+  void* wfr = nullptr;                  // pair path: per-ray arrays (nearest hit, hit point, shadow counts), grow-only
+  size_t wfr_bytes = 0;
+  void* wfp = nullptr;                  // pair path: pair lists + sort scratch, grow-only
+  size_t wfp_bytes = 0;
+  uint32_t wfp_cap = 0;
   // Cost-ordered tile dispatch.  A frame's time is set by its slowest tiles (long reflection
   // chains), so they are dispatched first: the first launch of a geometry records every tile's
   // wave time, and later launches of the same geometry read the tiles in descending cost order.
@@ -2203,6 +2582,8 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   d.shadow_early_out = f.shadow_early_out;
   d.colour_fast = f.colour_fast;
   d.ray_chains = f.ray_chains;
+  d.shadow_pow = f.shadow_pow;
+  d.shadow_t = f.shadow_t;
   d.cam = f.cam;
   c->max_depth = f.max_depth;
   {                                   // the wavefront path's key extent: the hull of the bounded objects
@@ -2221,9 +2602,126 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   return RT_OK;
 }
 
+extern "C" hipError_t rt_wf_bucket_sort(const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
+                                        uint32_t* vals_out, uint32_t n, uint32_t nb, int shift, uint32_t* cnt,
+                                        hipStream_t stream);
 extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                                        const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit,
                                        hipStream_t stream);
+
+// Pair-path arrays (render_kernels.hip "wavefront pair path"): per ray of a level (R = the larger of
+// the pixel slots and the level capacity) and, grow-only, the pair lists for `need` pairs.
+static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t need, WfPairs* P) {
+  const size_t nl = (size_t)std::max(1, c->dev.n_lights);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_omin = al(R * 8), o_px = al(o_omin + R * 4), o_k = al(o_px + 3 * R * 8), o_q = al(o_k + R * nl * 4);
+  const size_t o_h = al(o_q + R * nl * 4), rbytes = al(o_h + 4 * R * 4);
+  if (c->wfr_bytes < rbytes) {
+    if (c->wfr) (void)hipFree(c->wfr);
+    c->wfr = nullptr;
+    c->wfr_bytes = 0;
+    RT_HIP(hipMalloc(&c->wfr, rbytes));
+    c->wfr_bytes = rbytes;
+  }
+  if (need > c->wfp_cap || !c->wfp) {
+    const size_t cap = std::min<size_t>(0x7fffffc0ull, std::max<size_t>(need + need / 4, 8 * R) + 63) & ~(size_t)63;
+    if (need > cap) return fail(RT_ERR_UNSUPPORTED, "wavefront pair list of %zu pairs too large", need);
+    size_t sort_bytes = 0;
+    RT_HIP(rt_wf_sort_pairs(nullptr, &sort_bytes, nullptr, nullptr, nullptr, nullptr, (int)cap, 32, st));
+    const size_t bytes = al(256 + 16384 + 4 * cap * 4 + cap * 8) + sort_bytes + 256;
+    if (c->wfp) (void)hipFree(c->wfp);    // waits for launches that may still use it
+    c->wfp = nullptr;
+    c->wfp_bytes = 0;
+    c->wfp_cap = 0;
+    RT_HIP(hipMalloc(&c->wfp, bytes));
+    c->wfp_bytes = bytes;
+    c->wfp_cap = (uint32_t)cap;
+  }
+  uint8_t* r = (uint8_t*)c->wfr;
+  P->tmin = (unsigned long long*)r;
+  P->omin = (int32_t*)(r + o_omin);
+  P->px = (double*)(r + o_px);
+  P->py = P->px + R;
+  P->pz = P->py + R;
+  P->kcnt = (uint32_t*)(r + o_k);
+  P->opq = (uint32_t*)(r + o_q);
+  P->hkey = (uint32_t*)(r + o_h);
+  P->hval = P->hkey + R;
+  P->hkey_s = P->hval + R;
+  P->hperm = P->hkey_s + R;
+  uint8_t* b = (uint8_t*)c->wfp;
+  const size_t cap = c->wfp_cap;
+  P->cap = (uint32_t)cap;
+  P->count = (uint32_t*)b;
+  P->bins = (uint32_t*)(b + 256);
+  P->key = (uint32_t*)(b + 256 + 16384);
+  P->val = P->key + cap;
+  P->key_s = P->val + cap;
+  P->val_s = P->key_s + cap;
+  P->tp = (double*)(P->val_s + cap);
+  return RT_OK;
+}
+
+// One level of the wavefront path through the pair path: candidate pairs, sort by object, pair
+// evaluation and the folds, for the nearest hits and then the shadow rays, then the shading pass.
+// The host reads each pair count (a synchronisation): the sort and the evaluation grids are exact,
+// and a count beyond the arena grows it and re-runs the candidate pass.
+static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int d, uint32_t n, int a0, int a1,
+                     int a2, int a3, int max_depth, bool refr, bool fc) {
+  WfPairs P;
+  int rc = wfp_arena(c, st, R, 0, &P);
+  if (rc) return rc;
+  int obits = 1;
+  while (obits < 32 && (1u << obits) < (uint32_t)c->dev.n_objects) ++obits;
+  const dim3 g((n + 63) / 64), b64(64);
+  for (int pass = 0; pass < 2; ++pass) {
+    uint32_t np = 0;
+    if (pass == 1) {                  // the hit points and their order for the shadow and shading passes
+      hipLaunchKernelGGL(wfp_hit_key_kernel, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, c->dev,
+                         A, P, d, n, a0, a1, a2, a3);
+      size_t tb = c->wfp_bytes - (size_t)((uint8_t*)(P.tp + P.cap) - (uint8_t*)c->wfp) - 256;
+      void* tmp = (void*)(((uintptr_t)(P.tp + P.cap) + 255) & ~(uintptr_t)255);
+      // 4096 buckets of the key's top 12 bits (a 16^3 grid of hit-point cells), unordered within a
+      // bucket: 0.4 ms per fractal frame faster than the full 27-bit radix sort (rocPRIM's small-size
+      // path is a dozen merge launches), profiles/r03o_sort_ab.txt
+      RT_HIP(rt_wf_bucket_sort(P.hkey, P.hkey_s, P.hval, P.hperm, n, 4096, 15, P.bins, st));
+      (void)tb;
+      (void)tmp;
+    }
+    for (;;) {
+      RT_HIP(hipMemsetAsync(P.count, 0, 4, st));
+      if (pass == 0) hipLaunchKernelGGL((wfp_cand_kernel<false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+      else hipLaunchKernelGGL((wfp_cand_kernel<true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+      RT_HIP(hipGetLastError());
+      RT_HIP(hipMemcpyAsync(&np, P.count, 4, hipMemcpyDeviceToHost, st));
+      RT_HIP(hipStreamSynchronize(st));
+      if (np <= P.cap) break;
+      rc = wfp_arena(c, st, R, np, &P);
+      if (rc) return rc;
+    }
+    if (np == 0) continue;
+    size_t tb = c->wfp_bytes - (size_t)((uint8_t*)(P.tp + P.cap) - (uint8_t*)c->wfp) - 256;
+    void* tmp = (void*)(((uintptr_t)(P.tp + P.cap) + 255) & ~(uintptr_t)255);
+    if (c->dev.n_objects <= 4096)
+      RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, np, (uint32_t)c->dev.n_objects, 0, P.bins, st));
+    else
+      RT_HIP(rt_wf_sort_pairs(tmp, &tb, P.key, P.key_s, P.val, P.val_s, (int)np, obits, st));
+    const dim3 ge((np + 63) / 64);
+    if (pass == 0) {
+      hipLaunchKernelGGL(wfp_near_eval_kernel, ge, b64, 0, st, c->dev, A, P, d, np, a0, a1, a2, a3);
+      hipLaunchKernelGGL(wfp_near_tie_kernel, dim3(std::min<uint32_t>((np + 255) / 256, 4096)), dim3(256), 0, st, P, np);
+    } else {
+      hipLaunchKernelGGL(wfp_shadow_eval_kernel, ge, b64, 0, st, c->dev, P, np);
+    }
+    RT_HIP(hipGetLastError());
+  }
+  if (refr && fc) hipLaunchKernelGGL((wfp_shade_kernel<true, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
+  else if (refr) hipLaunchKernelGGL((wfp_shade_kernel<true, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
+  else if (fc) hipLaunchKernelGGL((wfp_shade_kernel<false, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
+  else hipLaunchKernelGGL((wfp_shade_kernel<false, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}
 
 // The wavefront path (wf_*_kernel): level 0 (the pixel slots), then each level the previous one
 // appended to, sorted by coherence key; then the folds, deepest level first; then the overflow
@@ -2263,6 +2761,8 @@ static int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, i
   RT_HIP(hipMemsetAsync(A.count, 0, 256, st));
   RT_HIP(hipMemsetAsync(A.ovf, 0, slots, st));
   const bool refr = c->dev.any_transparent != 0, fc = c->dev.colour_fast != 0 && c->fast_clamp;
+  const bool pairs = c->wf_pairs > 0 && c->dev.shadow_pow != 0 && c->dev.n_objects > 0;
+  auto pairs_level = [&](int d) { return pairs && (d > 0 || c->wf_pairs == 2); };
   uint32_t n_level[RT_MAX_DEPTH_CAP + 2] = {0};
   n_level[0] = (uint32_t)slots;
   int last = 0;
@@ -2273,12 +2773,21 @@ static int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, i
     A.perm = nullptr;
     if (d > 0) {                                             // this level's slots in key order
       const WfLevel L = wf_level(A, d);                      // host-side pointer arithmetic only
-      size_t tb = sort_bytes;
-      RT_HIP(rt_wf_sort_pairs(tmp, &tb, L.key, kout, L.val, perm, (int)n, 30, st));
-      A.perm = perm;
+      // The pair path reads a level in slot order: its candidate walks are per lane and its
+      // evaluations run in object order, and the sort measured 0.3-0.6 ms per fractal frame slower
+      // than none (profiles/r03o_sort_ab.txt).
+      if (!pairs_level(d)) {
+        size_t tb = sort_bytes;
+        RT_HIP(rt_wf_sort_pairs(tmp, &tb, L.key, kout, L.val, perm, (int)n, 30, st));
+        A.perm = perm;
+      }
     }
     const dim3 g((n + 63) / 64);
-    if (refr && fc) hipLaunchKernelGGL((wf_trace_kernel<true, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    if (pairs_level(d)) {
+      int rc = wfp_level(c, st, A, std::max(slots, cap), d, n, a0, a1, a2, a3, max_depth, refr, fc);
+      if (rc) return rc;
+    }
+    else if (refr && fc) hipLaunchKernelGGL((wf_trace_kernel<true, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
     else if (refr) hipLaunchKernelGGL((wf_trace_kernel<true, false>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
     else if (fc) hipLaunchKernelGGL((wf_trace_kernel<false, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
     else hipLaunchKernelGGL((wf_trace_kernel<false, false>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
@@ -2857,6 +3366,11 @@ int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
     c->timed = false;                  // no launch recorded under the new setting yet
     return RT_OK;
   }
+  if (option == RT_OPT_WAVEFRONT_PAIRS) {
+    if (value < 0 || value > 2) return fail(RT_ERR_INVALID, "RT_OPT_WAVEFRONT_PAIRS %d not in [0, 2]", value);
+    c->wf_pairs = value;
+    return RT_OK;
+  }
   if (option == RT_OPT_WAVEFRONT_CAP) {
     if (value < 1 || value > 400) return fail(RT_ERR_INVALID, "RT_OPT_WAVEFRONT_CAP %d not in [1, 400]", value);
     c->wf_cap_pct = value;
@@ -2922,6 +3436,8 @@ void rt_ctx_free(rt_ctx* c) {
   if (c->d_blob) (void)hipFree(c->d_blob);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->wf) (void)hipFree(c->wf);
+  if (c->wfr) (void)hipFree(c->wfr);
+  if (c->wfp) (void)hipFree(c->wfp);
   drop_orders(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);

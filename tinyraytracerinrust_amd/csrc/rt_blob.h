@@ -145,10 +145,11 @@ struct alignas(16) RtObject {
 // skips to `skip`.  Objects are still visited in increasing index order, so the nearest-hit tie
 // rule (first object wins) and the shadow product order are the reference's.
 struct alignas(16) RtTrav {
-  double blo[3], bhi[3];
+  double blo[3], bhi[3];            // group: hull of its objects' boxes; object node: a copy of the object's box
   int32_t obj;                      // >= 0: object index; -1: group node
   int32_t skip;                     // node index after this node's subtree
-  int32_t pad[2];
+  int32_t cull;                     // object node: a copy of RtObject::cull (one record per step of a
+  int32_t shadow_skip;              //   per-lane walk, render_kernels.hip wfp_cand_kernel), ::shadow_skip
 };
 
 struct RtTexture {
@@ -180,5 +181,9 @@ struct RtDevScene {
   int32_t shadow_early_out;         // every transparency is finite: product==0 stays 0
   int32_t colour_fast;              // colour clamps may take the min/max form (render_kernels.hip FC)
   int32_t ray_chains;               // every hit spawns at most one ray (scene.cpp flatten)
+  int32_t shadow_pow;               // a shadow product depends only on its factors' multiset: every
+                                    // transparency is finite and all those other than +-0 and 1 are
+                                    // one value, shadow_t (scene.cpp flatten; the wavefront pair path)
+  double shadow_t;
   RtCamera cam;
 };

@@ -594,6 +594,10 @@ struct HierBuilder {
     memset(&t, 0, sizeof t);
     t.obj = perm[o];
     t.skip = (int32_t)out.size() + 1;
+    const RtObject& ob = f.objects[perm[o]];
+    for (int k = 0; k < 3; ++k) { t.blo[k] = ob.blo[k]; t.bhi[k] = ob.bhi[k]; }
+    t.cull = ob.cull;
+    t.shadow_skip = ob.shadow_skip;
     out.push_back(t);
   }
   // Positions [a, b), all objects with a finite box.  A group node is emitted when it is clearly
@@ -695,6 +699,15 @@ int flatten(const rt_scene& s, FlatScene* out) {
   // comparisons: a NaN counts as nonzero), a refracted hit has rp = refl = +-0 (no reflection) and a
   // TIR hit has no refraction: every hit spawns at most one ray, so each pixel's rays form a chain.
   f.ray_chains = 1;
+  // shadow_pow: a shadow ray's transparency is the product, in draw order, of the transparency of
+  // every filtered hit in range, 0 at the first +-0 factor (raytracer.rs:181-197; objects of
+  // transparency 1 are skipped).  When every other factor is ONE value T, the product is
+  // fl(...fl(fl(1 * T) * T)...) over however many there are -- it depends on the count of T hits and
+  // on whether a +-0 hit exists, not on their order -- so the wavefront pair path may evaluate
+  // (shadow ray, object) pairs in any order and fold counts (render_kernels.hip wfp_*).
+  f.shadow_pow = 1;
+  f.shadow_t = 0.0;
+  bool have_t = false;
   auto nonneg = [](double x) { return std::isfinite(x) && !std::signbit(x); };
   auto unit = [&](double x) { return nonneg(x) && x <= 1.0; };
   for (const ObjectRec& o : s.objects) {
@@ -762,10 +775,15 @@ int flatten(const rt_scene& s, FlatScene* out) {
     if (m.transparency != 0.0) f.any_transparent = 1;
     if (m.transparency != 0.0 && m.reflectivity != 0.0) f.ray_chains = 0;
     if (!isfinite(m.transparency)) f.shadow_early_out = 0;
+    if (m.transparency != 0.0 && m.transparency != 1.0) {
+      if (!have_t) { f.shadow_t = m.transparency; have_t = true; }
+      else if (memcmp(&f.shadow_t, &m.transparency, sizeof(double)) != 0) f.shadow_pow = 0;
+    }
     if (!unit(m.reflectivity) || !unit(m.transparency)) f.colour_fast = 0;
     if (m.texture < 0 && !(nonneg(m.color[0]) && nonneg(m.color[1]) && nonneg(m.color[2]))) f.colour_fast = 0;
     f.objects.push_back(ob);
   }
+  if (!f.shadow_early_out) f.shadow_pow = 0;
   for (RtObject& ob : f.objects) share_sphere_terms(f, &ob);
   {
     std::vector<int> draw((size_t)f.objects.size());
@@ -789,8 +807,8 @@ int flatten(const rt_scene& s, FlatScene* out) {
     while (off % 16) { f.texels.push_back(0); ++off; }
   }
   if (getenv("RT_DUMP_FLAT")) {                                // debugging aid: culling boxes
-    fprintf(stderr, "scene any_transparent=%d ray_chains=%d colour_fast=%d shadow_early_out=%d\n", f.any_transparent,
-            f.ray_chains, f.colour_fast, f.shadow_early_out);
+    fprintf(stderr, "scene any_transparent=%d ray_chains=%d colour_fast=%d shadow_early_out=%d shadow_pow=%d\n",
+            f.any_transparent, f.ray_chains, f.colour_fast, f.shadow_early_out, f.shadow_pow);
     for (size_t i = 0; i < f.trav.size(); ++i)
       fprintf(stderr, "trav %zu obj=%d skip=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f]\n", i, f.trav[i].obj, f.trav[i].skip,
               f.trav[i].blo[0], f.trav[i].blo[1], f.trav[i].blo[2], f.trav[i].bhi[0], f.trav[i].bhi[1], f.trav[i].bhi[2]);

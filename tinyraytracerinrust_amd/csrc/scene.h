@@ -53,6 +53,8 @@ struct FlatScene {
   int32_t any_transparent, shadow_early_out;
   int32_t colour_fast;   // every colour-op operand is finite and >= +0 (see flatten)
   int32_t ray_chains;    // every hit spawns at most one ray: no object is both transparent and reflective
+  int32_t shadow_pow;    // shadow products are order-free (see RtDevScene::shadow_pow)
+  double shadow_t;
 };
 
 // Transformation math (transformation.rs:104-220), exact f64 op order.

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
+#include <algorithm>
 
 // d_temp == nullptr: *temp_bytes = the scratch the sort of n pairs needs.  Sorts bits [0, end_bit).
 extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
@@ -11,4 +12,101 @@ extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const u
                                        hipStream_t stream) {
   return hipcub::DeviceRadixSort::SortPairs(d_temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out, n, 0, end_bit,
                                             stream);
+}
+
+// ---------------------------------------------------------------------------- bucket sort
+// The pair path's sort of (object, pair) by object: few keys (the scene's objects), many items.  A
+// counting sort in three launches (a radix sort of a few million items takes a dozen: rocPRIM's
+// block sort + merge passes below its one-sweep size), not stable -- the pair order within an
+// object does not matter (render_kernels.hip wfp_*: the folds are atomic min / add / or).
+//   hist:    per workgroup an LDS histogram of its grid-stride share, added to cnt[] (one atomic per
+//            nonzero bin and workgroup);
+//   scan:    one workgroup turns cnt[] into exclusive offsets in place;
+//   scatter: per workgroup a contiguous chunk: LDS counts give each item its rank among the chunk's
+//            items of its key, one atomic per nonzero bin reserves the chunk's run in that bucket.
+#define RT_BS_MAX_BINS 4096
+#define RT_BS_THREADS 256
+#define RT_BS_PER_THREAD 16
+__device__ __forceinline__ uint32_t rt_bs_bin(uint32_t key, int shift, uint32_t nb) {
+  return min(key >> shift, nb - 1u);
+}
+__global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t nb,
+                                                           int shift, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t h[RT_BS_MAX_BINS];
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    atomicAdd(&h[rt_bs_bin(keys[i], shift, nb)], 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+    if (h[b]) atomicAdd(&cnt[b], h[b]);
+}
+
+__global__ __launch_bounds__(1024) void rt_bs_scan(uint32_t* __restrict__ cnt, uint32_t nb) {
+  __shared__ uint32_t part[1024];
+  const uint32_t per = (nb + 1023) / 1024, b0 = threadIdx.x * per;
+  uint32_t s = 0;
+  for (uint32_t b = b0; b < b0 + per && b < nb; ++b) s += cnt[b];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {          // inclusive scan of the thread sums
+    const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[threadIdx.x] - s;
+  for (uint32_t b = b0; b < b0 + per && b < nb; ++b) {
+    const uint32_t c = cnt[b];
+    cnt[b] = run;
+    run += c;
+  }
+}
+
+__global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_scatter(const uint32_t* __restrict__ keys,
+                                                              const uint32_t* __restrict__ vals, uint32_t n,
+                                                              uint32_t nb, int shift, uint32_t* __restrict__ off,
+                                                              uint32_t* __restrict__ keys_out,
+                                                              uint32_t* __restrict__ vals_out) {
+  __shared__ uint32_t h[RT_BS_MAX_BINS];
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * (RT_BS_THREADS * RT_BS_PER_THREAD);
+  uint32_t k[RT_BS_PER_THREAD], r[RT_BS_PER_THREAD];
+#pragma unroll
+  for (int e = 0; e < RT_BS_PER_THREAD; ++e) {
+    const uint32_t i = base + (uint32_t)e * RT_BS_THREADS + threadIdx.x;
+    k[e] = i < n ? rt_bs_bin(keys[i], shift, nb) : 0u;
+    r[e] = i < n ? atomicAdd(&h[k[e]], 1u) : 0u;
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+    if (h[b]) h[b] = atomicAdd(&off[b], h[b]);              // this chunk's run in bucket b
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < RT_BS_PER_THREAD; ++e) {
+    const uint32_t i = base + (uint32_t)e * RT_BS_THREADS + threadIdx.x;
+    if (i < n) {
+      const uint32_t q = h[k[e]] + r[e];
+      keys_out[q] = k[e];
+      vals_out[q] = vals[i];
+    }
+  }
+}
+
+// Sorts n (key, value) pairs by bin = min(key >> shift, nb - 1) (nb <= RT_BS_MAX_BINS) into keys_out
+// (the bins) / vals_out; cnt: nb words of device scratch.
+extern "C" hipError_t rt_wf_bucket_sort(const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
+                                        uint32_t* vals_out, uint32_t n, uint32_t nb, int shift, uint32_t* cnt,
+                                        hipStream_t stream) {
+  if (nb == 0 || nb > RT_BS_MAX_BINS) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nb * 4, stream);
+  if (e != hipSuccess) return e;
+  const uint32_t chunk = RT_BS_THREADS * RT_BS_PER_THREAD, gh = std::min<uint32_t>((n + chunk - 1) / chunk, 2048u);
+  hipLaunchKernelGGL(rt_bs_hist, dim3(gh), dim3(RT_BS_THREADS), 0, stream, keys_in, n, nb, shift, cnt);
+  hipLaunchKernelGGL(rt_bs_scan, dim3(1), dim3(1024), 0, stream, cnt, nb);
+  hipLaunchKernelGGL(rt_bs_scatter, dim3((n + chunk - 1) / chunk), dim3(RT_BS_THREADS), 0, stream, keys_in, vals_in, n,
+                     nb, shift, cnt, keys_out, vals_out);
+  return hipGetLastError();
 }

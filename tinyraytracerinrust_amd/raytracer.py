@@ -302,6 +302,12 @@ class Renderer:
         percent of the launch's pixel slots (pixels whose tree overflows are re-rendered, same bits)."""
         check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_WAVEFRONT_CAP, int(percent)))
 
+    def set_wavefront_pairs(self, mode: int) -> None:
+        """rt_ctx_set_option(RT_OPT_WAVEFRONT_PAIRS): the wavefront path's per-level tracing: 0 one wave
+        walks the hierarchy for 64 rays, 1 (default) levels >= 1 as (ray, object) pairs sorted by
+        object, 2 every level (same pixels)."""
+        check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_WAVEFRONT_PAIRS, int(mode)))
+
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()
         check(lib().rt_ctx_last_kernel_ms(self.h, ctypes.byref(ms)))

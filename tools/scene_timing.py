@@ -2,7 +2,7 @@
 bench.py is the contract).  One context per (depth, kernel); the first launch calibrates, then
 REPS ordered launches are timed with the library's launch events (median printed).
 usage: python tools/scene_timing.py SCENE WxH TIME DEPTHS [KERNELS] [REPS]
-  e.g. python tools/scene_timing.py fractal 1920x1080 0 0,1,2,4,10 auto,mega 5"""
+  e.g. python tools/scene_timing.py fractal 1920x1080 0 0,1,2,4,10 auto,mega,wavefront:p0,wavefront:p2 5"""
 import os
 import statistics
 import sys
@@ -24,7 +24,10 @@ for d in depths:
         rt.max_depth = d
         rt.load_scene(text, t, asset_dir=S)
         r = rt.renderer
-        r.set_kernel(k)
+        kn, _, pm = k.partition(":p")                     # e.g. wavefront:p0 = RT_OPT_WAVEFRONT_PAIRS 0
+        r.set_kernel(kn)
+        if pm:
+            r.set_wavefront_pairs(int(pm))
         out = r.render_rows(0, H)
         torch.cuda.synchronize()
         cal = r.last_kernel_ms()
