@@ -135,7 +135,11 @@ namespace {
 
 // Scene tables are read-only for the whole launch: view them through the CONSTANT address space
 // (4) so uniform-index reads compile to scalar (SMEM) loads instead of per-lane VMEM loads.
+#ifdef RT_DIAG_LDS_SCENE                 // diagnostic A/B build only (make diag): scene tables staged in LDS
+#define CAS __attribute__((address_space(3)))
+#else
 #define CAS __attribute__((address_space(4)))
+#endif
 template <class T> using cptr = const CAS T*;
 template <class T> __device__ __forceinline__ cptr<T> as_const(const T* p) { return (cptr<T>)p; }
 
@@ -1259,8 +1263,13 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
 // Workgroup = one wave of 8x8 pixels: measured 3-5 % faster than 2x2-wave workgroups (round 1).
 constexpr int RT_WG_THREADS = 64;
 constexpr int RT_TILE_W = 8, RT_TILE_H = 8;
+#ifdef RT_DIAG_LDS_SCENE
+#define RT_ROWS_WG_THREADS 256
+#else
+#define RT_ROWS_WG_THREADS RT_WG_THREADS
+#endif
 template <int MODE, bool F64, bool CAL = false, bool FC = false>
-__global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(RT_WAVES_MODE(MODE)))) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
+__global__ __launch_bounds__(RT_ROWS_WG_THREADS) __attribute__((amdgpu_waves_per_eu(RT_WAVES_MODE(MODE)))) void render_rows_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch,
                                                           int n_rows, int max_depth, uint8_t* __restrict__ out,
                                                           size_t stride, const int32_t* __restrict__ order,
                                                           uint32_t* __restrict__ cost, int rgb) {
@@ -1270,10 +1279,25 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
   if (threadIdx.x == 0) rt_pad[0] = 0;
 #endif
   const int lane = threadIdx.x & 63;
+#ifdef RT_DIAG_LDS_SCENE
+  // Diagnostic A/B (the north star's "node arrays staged in LDS"): 4 waves per workgroup share one
+  // LDS copy of the scene tables (objects .. texture headers); every scene read below is then an LDS
+  // read (ds_read, the same address on every lane) instead of a scalar load.
+  constexpr int WPB = 4;
+  const unsigned wave = threadIdx.x >> 6, entry = blockIdx.x * WPB + wave;
+  __shared__ __attribute__((aligned(16))) uint8_t s_scene[RT_DIAG_LDS_SCENE];
+  const uint8_t* b0 = (const uint8_t*)S.objects;
+  const size_t nbytes = (size_t)(S.texels - b0);
+  for (size_t q = threadIdx.x * 16; q < nbytes && q + 16 <= RT_DIAG_LDS_SCENE; q += WPB * 64 * 16)
+    *(uint4*)&s_scene[q] = *(const uint4*)&b0[q];
+  __syncthreads();
+  const unsigned tile = CAL || !order ? entry : (unsigned)order[entry];
+#else
   // Tile dispatch order (see launch_bands): `order` lists the tiles most expensive first, as
   // measured on a calibration launch that stored each tile's wave time in `cost`.
   // CAL (the calibration instantiation) is the only one that carries the timing code.
   const unsigned tile = CAL || !order ? blockIdx.x : (unsigned)order[blockIdx.x];
+#endif
 #ifdef RT_DIAG_HOT_TILES                 // diagnostic A/B builds only: issue priority for the costliest tiles
   if (!CAL && order && blockIdx.x < RT_DIAG_HOT_TILES) __builtin_amdgcn_s_setprio(3);
 #endif
@@ -1292,9 +1316,28 @@ __global__ __launch_bounds__(RT_WG_THREADS) __attribute__((amdgpu_waves_per_eu(R
 #if RT_LDS_FRAMES > 0
   constexpr int KLR = MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0;
   constexpr int KL = CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES;
+#ifdef RT_DIAG_LDS_SCENE
+  __shared__ double s_frames[WPB][(KL * 4 + KLR * 7) * 64];
+  lds_f64* lf = (lds_f64*)&s_frames[wave][lane];
+  DS D = make_ds(S);
+  {
+    CAS uint8_t* L0 = (CAS uint8_t*)s_scene;
+    auto lds = [&](const void* p) { return L0 + ((const uint8_t*)p - b0); };
+    D.objects = (cptr<RtObject>)lds(S.objects);
+    D.trav = (cptr<RtTrav>)lds(S.trav);
+    D.strav = (cptr<RtTrav>)lds(S.strav);
+    D.nodes = (cptr<RtNode>)lds(S.nodes);
+    D.leaves = (cptr<RtLeaf>)lds(S.leaves);
+    D.prog = (cptr<RtProg>)lds(S.prog);
+    D.lights = (cptr<RtLight>)lds(S.lights);
+    D.textures = (cptr<RtTexture>)lds(S.textures);
+  }
+  const Col c = trace<REFR, NoRec, KL, FC, KLR, CHAIN>(D, ro, rd, max_depth, nullptr, lf);
+#else
   __shared__ double s_frames[(KL * 4 + KLR * 7) * 64];   // frame stack, see trace()
   lds_f64* lf = (lds_f64*)&s_frames[lane];
   const Col c = trace<REFR, NoRec, KL, FC, KLR, CHAIN>(make_ds(S), ro, rd, max_depth, nullptr, lf);
+#endif
 #else
   const Col c = trace<REFR, NoRec, 0, FC, 0, CHAIN>(make_ds(S), ro, rd, max_depth);
 #endif
@@ -2894,7 +2937,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
         if (s.last_use < slot->last_use) slot = &s;
       }
       drop_order(*slot);
-      RT_HIP(hipMalloc((void**)&slot->d_order, n_tiles * sizeof(int32_t)));
+      RT_HIP(hipMalloc((void**)&slot->d_order, (n_tiles + 4) * sizeof(int32_t)));   // + 4: RT_DIAG_LDS_SCENE groups
       RT_HIP(hipMalloc((void**)&slot->d_cost, n_tiles * sizeof(uint32_t)));
       RT_HIP(hipMemsetAsync(slot->d_cost, 0, n_tiles * sizeof(uint32_t), st));   // tiles that store no cost sort last
       memcpy(slot->key, key, sizeof(key));
@@ -2907,6 +2950,12 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   const int32_t* order = slot && !calibrate ? slot->d_order : nullptr;
   uint32_t* cost = calibrate ? slot->d_cost : nullptr;
   if (order) grid.x = slot->grid;
+#ifdef RT_DIAG_LDS_SCENE
+  const dim3 grid_tiles = grid;
+  grid.x = (grid.x + 3) / 4;                     // 4 tiles per 256-thread workgroup (render_rows_kernel)
+  block.x = 256;
+  (void)grid_tiles;
+#endif
   bool deferred;
   if (!eligible || dmode == 0) deferred = false;
   else if (dmode == 1) deferred = true;
@@ -3032,6 +3081,9 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
       }
     }
     slot->grid = (uint32_t)h_order.size();
+#ifdef RT_DIAG_LDS_SCENE
+    if (!slot->deferred) h_order.resize(h_order.size() + 4, -1);   // entries past the last tile: no tile
+#endif
     RT_HIP(hipMemcpyAsync(slot->d_order, h_order.data(), h_order.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
     RT_HIP(hipStreamSynchronize(st));
     slot->valid = true;

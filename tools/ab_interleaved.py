@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--upload-env", nargs="*", default=[],
                     help="per library (in order): KEY=VAL set in the environment while its scene is compiled and "
                          "uploaded (host-side flattening switches, e.g. RT_NO_LIT_ORDER=1); '-' for none")
+    ap.add_argument("--check", action="store_true",
+                    help="after timing, render once more per library and require every frame to equal the first's")
     ap.add_argument("--kernel", nargs="*", default=[],
                     help="per library (in order): RT_OPT_KERNEL auto / mega / deferred for its context; '-' keeps auto. "
                          "A library path may repeat with different kernels")
@@ -71,6 +73,19 @@ def main():
             L.rt_ctx_last_kernel_ms(cx, ctypes.byref(v))
             if rep >= 3:
                 ms.append(v.value if a.burst == 1 else dt)
+    if a.check:
+        frames = []
+        for path, L, cx, ms in ctxs:
+            o = torch.zeros_like(out)
+            assert L.rt_render_rows(cx, 0, H, a.depth, ctypes.c_void_p(o.data_ptr()), ctypes.c_size_t(W * 4),
+                                    ctypes.c_void_p(st)) == 0
+            torch.cuda.synchronize()
+            frames.append(o)
+        for (path, *_), f in zip(ctxs[1:], frames[1:]):
+            same = bool(torch.equal(f, frames[0]))
+            print(f"check: {path} frame {'==' if same else '!='} {ctxs[0][0]} frame", flush=True)
+            if not same:
+                return 1
     base = None
     for path, L, cx, ms in ctxs:
         med = statistics.median(ms)
