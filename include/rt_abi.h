@@ -193,6 +193,13 @@ int rt_render_rows_f64(rt_ctx* ctx, uint32_t y0, uint32_t y1, int32_t max_depth,
  * antialiaser.rs:108-112): xy = n pairs of doubles, out = n x 4 doubles. Device or host. */
 int rt_render_points_f64(rt_ctx* ctx, const double* xy, size_t n, int32_t max_depth,
                          double* rgba_f64, void* stream);
+/* One sample of a scene without a context of the caller's: RayTracer::get_pixel(x, y)
+ * (raytracer.rs:359-365) as SURVEY 8(b) sketches it for hosts that trace single pixels (a debugger
+ * UI, an anti-aliaser driven pixel by pixel).  Traced on the GPU (`device`, a context of the calling
+ * thread kept for the next call; the scene is uploaded on every call, so an edited scene is seen):
+ * about a millisecond per call -- batches belong in rt_render_points_f64.  max_depth < 0: the
+ * scene's.  rgba = 4 doubles, host memory. */
+int rt_trace_pixel_f64(const rt_scene* scene, double x, double y, int32_t max_depth, int device, double rgba[4]);
 /* Ray-debugger recording (RayDebugger::record_rays, ray_debugger.rs:92-137): trace pixel (x, y)
  * (fractional allowed) once with the debugger callback attached and return one record per ray in
  * the reference's callback order (a ray reports after its children).  *n_rays = rays traced

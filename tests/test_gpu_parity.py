@@ -176,6 +176,25 @@ def test_points_match_rows(T):
     assert np.max(np.abs(got - want)) <= F64_TOL
 
 
+def test_trace_pixel_without_context(T):
+    """rt_trace_pixel_f64 (SURVEY 8(b)'s scene-level get_pixel): the same doubles as the context's
+    points launch and the oracle's get_pixel, and an edited-then-recompiled scene is seen."""
+    from oracle import oracle as O
+    from tinyraytracerinrust_amd import raytracer as R
+    W, H = 64, 48
+    text = scene_text("globes")
+    sc = R.Scene.compile(text, 0.0, W, H, asset_dir=SCENES)
+    rt = T.RayTracer(W, H)
+    rt.load_scene(text, 0.0, asset_dir=SCENES)
+    ref = O.OracleScene(text, 0.0, W, H)
+    for x, y in [(10 + 1 / 9, 20 + 5 / 9), (33.5, 7.25), (0.0, 47.875), (31.0, 30.0)]:
+        got = sc.trace_pixel(x, y)
+        assert np.array_equal(got, rt.renderer.render_points(np.array([[x, y]]))[0])
+        assert np.max(np.abs(got - ref.get_pixel(x, y))) <= F64_TOL
+    sc2 = R.Scene.compile("draw(sphere(<0, 0, 0>, 30, red))", 0.0, W, H)
+    assert not np.array_equal(sc2.trace_pixel(31.0, 30.0), sc.trace_pixel(31.0, 30.0))
+
+
 def test_device_output_and_torch_stream(T):
     import torch
     W, H = 96, 64

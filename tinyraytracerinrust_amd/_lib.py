@@ -93,6 +93,7 @@ SIGNATURES = {
     "rt_assemble_row_bands_rgb8": (_I, [_P, ctypes.c_size_t, _U32, _U32, _U32, _U32, _U32, _P, ctypes.c_size_t, _P]),
     "rt_render_rows_f64": (_I, [_P, _U32, _U32, ctypes.c_int32, _P, ctypes.c_size_t, _P]),
     "rt_render_points_f64": (_I, [_P, _P, ctypes.c_size_t, ctypes.c_int32, _P, _P]),
+    "rt_trace_pixel_f64": (_I, [_P, ctypes.c_double, ctypes.c_double, ctypes.c_int32, ctypes.c_int, _P]),
     "rt_record_rays": (_I, [_P, ctypes.c_double, ctypes.c_double, ctypes.c_int32, _P, ctypes.c_int32,
                             ctypes.POINTER(ctypes.c_int32), _P]),
     "rt_render_ortho": (_I, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_double,

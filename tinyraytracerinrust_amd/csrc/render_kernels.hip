@@ -1369,6 +1369,11 @@ __global__ __launch_bounds__(RT_ROWS_WG_THREADS) __attribute__((amdgpu_waves_per
 #ifndef RT_WAVES_PER_EU_DEFERRED
 #define RT_WAVES_PER_EU_DEFERRED 7
 #endif
+#ifdef RT_DIAG_ENTRY_TIMES                // diagnostic build only: per dispatched entry, start / end ticks
+#define RT_ENTRY_TIMES_MAX (1 << 20)
+__device__ unsigned long long g_entry_times[RT_ENTRY_TIMES_MAX][2];
+__device__ unsigned g_diag_hot;             // entries below this index run at issue priority 3
+#endif
 template <bool F64, bool CAL = false, bool FC = false, bool REFR = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_DEFERRED))) void
 render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth,
@@ -1376,6 +1381,10 @@ render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_p
                             uint32_t* __restrict__ cost, int rgb) {
   __shared__ ShadowWin win;
   const int lane = threadIdx.x & 63;
+#ifdef RT_DIAG_ENTRY_TIMES
+  const unsigned long long et0 = wall_clock64();
+  if (!CAL && order && blockIdx.x < g_diag_hot) __builtin_amdgcn_s_setprio(3);
+#endif
   const uint32_t e = CAL || !order ? blockIdx.x : (uint32_t)order[blockIdx.x];
   const unsigned tile = e & RT_SPLIT_TILE_MASK;
   const int lp = (int)((e >> 24) & 7u), per = 64 >> lp;
@@ -1408,6 +1417,12 @@ render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_p
   }
   if constexpr (CAL)
     if (lane == 0) cost[tile] = (uint32_t)(wall_clock64() - t_start);
+#ifdef RT_DIAG_ENTRY_TIMES
+  if (!CAL && lane == 0 && blockIdx.x < RT_ENTRY_TIMES_MAX) {
+    g_entry_times[blockIdx.x][0] = et0;
+    g_entry_times[blockIdx.x][1] = wall_clock64();
+  }
+#endif
 }
 
 // ====================================================================== wavefront path
@@ -2535,6 +2550,18 @@ __attribute__((visibility("default"))) int rt_diag_cnt(unsigned long long* out64
 }
 #endif
 
+#ifdef RT_DIAG_ENTRY_TIMES
+// Diagnostic build only: start / end wall-clock ticks (100 MHz) of each entry of the last ordered
+// deferred launch, and the order itself (entry -> tile | part << 20 | log2 P << 24).
+__attribute__((visibility("default"))) int rt_diag_entry_times(rt_ctx* c, uint64_t* out, int32_t* order, size_t n) {
+  if (hipDeviceSynchronize() != hipSuccess) return RT_ERR_DEVICE;
+  if (n > RT_ENTRY_TIMES_MAX) n = RT_ENTRY_TIMES_MAX;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_entry_times), n * 16) != hipSuccess) return RT_ERR_DEVICE;
+  for (auto& s : c->order)
+    if (s.valid && s.deferred && s.grid >= n) return hipMemcpy(order, s.d_order, n * 4, hipMemcpyDeviceToHost) == hipSuccess ? 0 : RT_ERR_DEVICE;
+  return RT_ERR_INVALID;
+}
+#endif
 #ifdef RT_TILE_STATS
 // Diagnostic build only: the per-tile stats of the last calibration launch (4 words per tile).
 __attribute__((visibility("default"))) int rt_diag_tile_stats(uint32_t* out, size_t n_tiles) {
@@ -2973,6 +3000,14 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
                                   max_depth, target, tstride, order, cost, rgbi);                                       \
   else hipLaunchKernelGGL((render_rows_kernel<R, F, false, false>), grid, block, 0, st, c->dev, a0, a1, a2, a3,   \
                           max_depth, target, tstride, order, cost, rgbi);
+#ifdef RT_DIAG_ENTRY_TIMES
+  if (order && deferred) {                 // diagnostic: RT_DIAG_HOT=K priority entries, RT_DIAG_GRID=K first K only
+    const char* hv = getenv("RT_DIAG_HOT");
+    const unsigned hot = hv ? (unsigned)atoi(hv) : 0u;
+    RT_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_diag_hot), &hot, 4));
+    if (const char* gv = getenv("RT_DIAG_GRID")) grid.x = std::min<unsigned>(grid.x, (unsigned)atoi(gv));
+  }
+#endif
 #define RT_LAUNCH_DEFERRED(F, R)                                                                                \
   if (calibrate && fc) hipLaunchKernelGGL((render_rows_deferred_kernel<F, true, true, R>), grid, dim3(64), 0, st,    \
                                           c->dev, a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);     \
@@ -3367,6 +3402,28 @@ int rt_record_rays(rt_ctx* c, double x, double y, int32_t max_depth, rt_ray_reco
   for (int i = 0; i < keep; ++i) records[i] = rec[(size_t)ord[i]];
   if (rgba) for (int k = 0; k < 4; ++k) rgba[k] = rec[(size_t)dev_cap].color[k];
   return RT_OK;
+}
+
+int rt_trace_pixel_f64(const rt_scene* scene, double x, double y, int32_t max_depth, int device, double rgba[4]) {
+  if (!scene || !rgba) return fail(RT_ERR_INVALID, "null argument");
+  struct Holder {                       // the calling thread's context, freed with the thread
+    rt_ctx* c = nullptr;
+    ~Holder() { if (c) rt_ctx_free(c); }
+  };
+  static thread_local Holder h;
+  if (h.c && h.c->device != device) {
+    rt_ctx_free(h.c);
+    h.c = nullptr;
+  }
+  if (!h.c) {
+    int rc = rt_ctx_create(device, &h.c);
+    if (rc) return rc;
+    rt_ctx_set_option(h.c, RT_OPT_TIMING, 0);
+  }
+  int rc = rt_ctx_upload(h.c, scene);
+  if (rc) return rc;
+  const double xy[2] = {x, y};
+  return rt_render_points_f64(h.c, xy, 1, max_depth, rgba, nullptr);
 }
 
 int rt_render_points_f64(rt_ctx* c, const double* xy, size_t n, int32_t max_depth, double* out, void* stream) {

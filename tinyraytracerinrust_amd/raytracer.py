@@ -142,6 +142,14 @@ class Scene:
         return {"objects": no.value, "lights": nl.value, "leaves": nlf.value,
                 "width": w.value, "height": h.value}
 
+    def trace_pixel(self, x: float, y: float, max_depth: int = -1, device: int = 0) -> np.ndarray:
+        """rt_trace_pixel_f64: RayTracer::get_pixel(x, y) of this scene, traced on GPU ``device``
+        (no context of the caller's; one upload per call).  Returns 4 doubles (r, g, b, a)."""
+        out = np.empty(4, np.float64)
+        check(lib().rt_trace_pixel_f64(self.h, float(x), float(y), int(max_depth), int(device),
+                                       ctypes.c_void_p(out.ctypes.data)))
+        return out
+
     def traversal(self) -> List[Tuple[int, int]]:
         """The kernels' object hierarchy: pre-order (obj, skip) nodes, obj = -1 for a group."""
         n = ctypes.c_int32()
