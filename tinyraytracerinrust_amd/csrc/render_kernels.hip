@@ -2558,7 +2558,8 @@ __attribute__((visibility("default"))) int rt_diag_entry_times(rt_ctx* c, uint64
   if (n > RT_ENTRY_TIMES_MAX) n = RT_ENTRY_TIMES_MAX;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_entry_times), n * 16) != hipSuccess) return RT_ERR_DEVICE;
   for (auto& s : c->order)
-    if (s.valid && s.deferred && s.grid >= n) return hipMemcpy(order, s.d_order, n * 4, hipMemcpyDeviceToHost) == hipSuccess ? 0 : RT_ERR_DEVICE;
+    if (s.valid && s.deferred)
+      return hipMemcpy(order, s.d_order, std::min<size_t>(n, s.grid) * 4, hipMemcpyDeviceToHost) == hipSuccess ? 0 : RT_ERR_DEVICE;
   return RT_ERR_INVALID;
 }
 #endif
@@ -3094,7 +3095,10 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
       // (profiles/r02bo_split_sweep.txt): the 4K N = 8 share (16320 tiles) 0.150 / 0.152 / 0.172 /
       // 0.170 / 0.183 ms; the N = 4 share (32400 tiles) 0.209 / 0.192 / 0.190 / 0.200 / 0.232 ms;
       // the whole 1080p d5 frame (32400 tiles) 0.208 / 0.189 / 0.184 / 0.181 / 0.225 ms.
-      const double split_k = n_tiles < 24000 ? 1.0 : 1.5;
+      double split_k = n_tiles < 24000 ? 1.0 : 1.5;
+#ifdef RT_DIAG_ENTRY_TIMES
+      if (const char* kv = getenv("RT_DIAG_SPLIT_K")) split_k = atof(kv);
+#endif
       std::vector<uint32_t> sorted_cost(h_cost);
       std::nth_element(sorted_cost.begin(), sorted_cost.begin() + n_tiles / 2, sorted_cost.end());
       const double med = std::max(1.0, (double)sorted_cost[n_tiles / 2]);
