@@ -1759,7 +1759,8 @@ struct WfPairs {
   uint32_t *key, *val;          // pairs as emitted: object, ray id (level slot, or slot * n_lights + light)
   uint32_t *key_s, *val_s;      // sorted by object
   double* tp;                   // nearest pass: the sorted pair's object's nearest accepted distance
-  uint32_t* count;              // pairs emitted (may exceed cap: the host grows the arena and re-runs)
+  uint32_t* count;              // [0] / [1]: pairs the nearest / shadow pass emitted (may exceed cap: the host
+                                //   grows the arena and runs the level again)
   uint32_t* bins;               // bucket-sort scratch (RT_BS_MAX_BINS words)
   uint32_t cap;
   unsigned long long* tmin;     // per ray of the level: nearest accepted distance (bits; +inf: none)
@@ -1812,7 +1813,7 @@ __global__ __launch_bounds__(64) void wfp_cand_kernel(RtDevScene S, WfArena A, W
   auto flush = [&]() {
     __syncthreads();
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(P.count, nb);
+    if (lane == 0) base = atomicAdd(P.count + (SHADOW ? 1 : 0), nb);
     base = (uint32_t)__shfl((int)base, 0);
     for (uint32_t q = (uint32_t)lane; q < nb; q += 64)
       if (base + q < P.cap) { P.key[base + q] = sk[q]; P.val[base + q] = sv[q]; }
@@ -1937,36 +1938,40 @@ __device__ __forceinline__ uint32_t wfp_object_shadow(const DS& S, int o, V3 p, 
 
 // One lane per sorted pair: the waves see one object (two at a run boundary): scalarised over the
 // distinct objects of the wave as shade_inputs does, so every scene read is a scalar load.
-__global__ __launch_bounds__(64) void wfp_near_eval_kernel(RtDevScene S, WfArena A, WfPairs P, int d, uint32_t np,
-                                                           int y_first, int band_rows, int band_pitch, int n_rows) {
+__global__ __launch_bounds__(64) void wfp_near_eval_kernel(RtDevScene S, WfArena A, WfPairs P, int d, int y_first,
+                                                           int band_rows, int band_pitch, int n_rows) {
   const int lane = threadIdx.x & 63;
-  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+  const uint32_t np = min(P.count[0], P.cap);               // pairs of this level's nearest pass (device)
   const WfLevel lv = wf_level(A, d);
   const DS D = make_ds(S);
-  bool live = i < np;
-  uint32_t o = 0xffffffffu, j = 0;
-  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
-  if (live) {
-    o = P.key_s[i];
-    j = P.val_s[i];
-    live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
-  }
-  const CullRay cr = cull_ray(ro, rd);
-  double best = INFINITY;
-  uint64_t todo = __ballot(live);
-  while (todo) {
-    const uint32_t ou = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)__builtin_ctzll(todo));
-    const uint64_t mine = __ballot(live && o == ou);
-    todo &= ~mine;
-    if ((mine >> lane) & 1) best = wfp_object_nearest(D, (int)ou, ro, rd, cr);
-  }
-  if (live) {
-    P.tp[i] = best;
-    if (best < INFINITY) atomicMin(&P.tmin[j], (unsigned long long)__double_as_longlong(best));
+  for (uint32_t base = blockIdx.x * 64u; base < np; base += gridDim.x * 64u) {   // wave-uniform bounds
+    const uint32_t i = base + (uint32_t)lane;
+    bool live = i < np;
+    uint32_t o = 0xffffffffu, j = 0;
+    V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+    if (live) {
+      o = P.key_s[i];
+      j = P.val_s[i];
+      live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
+    }
+    const CullRay cr = cull_ray(ro, rd);
+    double best = INFINITY;
+    uint64_t todo = __ballot(live);
+    while (todo) {
+      const uint32_t ou = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)__builtin_ctzll(todo));
+      const uint64_t mine = __ballot(live && o == ou);
+      todo &= ~mine;
+      if ((mine >> lane) & 1) best = wfp_object_nearest(D, (int)ou, ro, rd, cr);
+    }
+    if (live) {
+      P.tp[i] = best;
+      if (best < INFINITY) atomicMin(&P.tmin[j], (unsigned long long)__double_as_longlong(best));
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void wfp_near_tie_kernel(WfPairs P, uint32_t np) {
+__global__ __launch_bounds__(256) void wfp_near_tie_kernel(WfPairs P) {
+  const uint32_t np = min(P.count[0], P.cap);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
     const double t = P.tp[i];
     if (!(t < INFINITY)) continue;
@@ -1976,57 +1981,62 @@ __global__ __launch_bounds__(256) void wfp_near_tie_kernel(WfPairs P, uint32_t n
 }
 
 // Per ray of the level, after the nearest-hit folds: the hit point (wf_ray_core's p) and a coherence
-// key for the shadow and shading passes, the Morton code of the hit point's cell (the light
-// directions from nearby points are alike, and nearby points mostly lie on the same object); misses
-// sort last.
+// key for the shadow and shading passes: the hit object above the top `cbits` bits of the Morton code
+// of the hit point's cell (a wave then shades one object -- shade_inputs' waterfall runs once -- and
+// its shadow rays start close together); misses sort last.
 __global__ __launch_bounds__(256) void wfp_hit_key_kernel(RtDevScene S, WfArena A, WfPairs P, int d, uint32_t n,
-                                                          int y_first, int band_rows, int band_pitch, int n_rows) {
+                                                          int y_first, int band_rows, int band_pitch, int n_rows,
+                                                          int cbits) {
   const WfLevel lv = wf_level(A, d);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t j = (d > 0 && A.perm) ? A.perm[i] : i;
     V3 ro, rd;
-    uint32_t key = 0xffffffffu;
+    uint32_t key = (uint32_t)S.n_objects << cbits;
     if (wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd) && P.omin[j] != 0x7fffffff) {
       const V3 p = add(ro, scale(rd, __longlong_as_double((long long)P.tmin[j])));
       P.px[j] = p.x; P.py[j] = p.y; P.pz[j] = p.z;
-      key = wf_key(A, p, V3{0.0, 0.0, 0.0}) & 0x07ffffffu;
+      const uint32_t cell = (wf_key(A, p, V3{0.0, 0.0, 0.0}) & 0x07ffffffu) >> (27 - cbits);
+      key = ((uint32_t)P.omin[j] << cbits) | (cbits ? cell : 0u);
     }
     P.hkey[i] = key;
     P.hval[i] = j;
   }
 }
 
-__global__ __launch_bounds__(64) void wfp_shadow_eval_kernel(RtDevScene S, WfPairs P, uint32_t np) {
+__global__ __launch_bounds__(64) void wfp_shadow_eval_kernel(RtDevScene S, WfPairs P) {
   const int lane = threadIdx.x & 63;
-  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+  const uint32_t np = min(P.count[1], P.cap);               // pairs of this level's shadow pass (device)
   const DS D = make_ds(S);
-  const bool live = i < np;
-  uint32_t o = 0xffffffffu, s = 0;
-  V3 p = {0.0, 0.0, 0.0}, sdir = {0.0, 0.0, 0.0};
-  double ll = 0.0;
-  if (live) {
-    o = P.key_s[i];
-    s = P.val_s[i];
-    const uint32_t j = s / (uint32_t)S.n_lights, k = s % (uint32_t)S.n_lights;
-    p = {P.px[j], P.py[j], P.pz[j]};
-    const RtLight& lt = S.lights[k];
-    const V3 l = sub(V3{lt.p[0], lt.p[1], lt.p[2]}, p);              // wf_ray_core's light loop
-    double ill;
-    len_inv(l, &ll, &ill);
-    sdir = scale(l, ill);
-  }
-  const CullRay cr = cull_ray(p, sdir);
-  uint32_t cnt = 0;
-  uint64_t todo = __ballot(live);
-  while (todo) {
-    const uint32_t ou = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)__builtin_ctzll(todo));
-    const uint64_t mine = __ballot(live && o == ou);
-    todo &= ~mine;
-    if ((mine >> lane) & 1) cnt = wfp_object_shadow(D, (int)ou, p, sdir, ll, cr);
-  }
-  if (live && cnt) {
-    if (D.objects[o].transparency == 0.0) atomicOr(&P.opq[s], 1u);
-    else atomicAdd(&P.kcnt[s], cnt);
+  for (uint32_t base = blockIdx.x * 64u; base < np; base += gridDim.x * 64u) {   // wave-uniform bounds
+    const uint32_t i = base + (uint32_t)lane;
+    const bool live = i < np;
+    uint32_t o = 0xffffffffu, s = 0;
+    V3 p = {0.0, 0.0, 0.0}, sdir = {0.0, 0.0, 0.0};
+    double ll = 0.0;
+    if (live) {
+      o = P.key_s[i];
+      s = P.val_s[i];
+      const uint32_t j = s / (uint32_t)S.n_lights, k = s % (uint32_t)S.n_lights;
+      p = {P.px[j], P.py[j], P.pz[j]};
+      const RtLight& lt = S.lights[k];
+      const V3 l = sub(V3{lt.p[0], lt.p[1], lt.p[2]}, p);              // wf_ray_core's light loop
+      double ill;
+      len_inv(l, &ll, &ill);
+      sdir = scale(l, ill);
+    }
+    const CullRay cr = cull_ray(p, sdir);
+    uint32_t cnt = 0;
+    uint64_t todo = __ballot(live);
+    while (todo) {
+      const uint32_t ou = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)__builtin_ctzll(todo));
+      const uint64_t mine = __ballot(live && o == ou);
+      todo &= ~mine;
+      if ((mine >> lane) & 1) cnt = wfp_object_shadow(D, (int)ou, p, sdir, ll, cr);
+    }
+    if (live && cnt) {
+      if (D.objects[o].transparency == 0.0) atomicOr(&P.opq[s], 1u);
+      else atomicAdd(&P.kcnt[s], cnt);
+    }
   }
 }
 
@@ -2674,15 +2684,15 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
 }
 
 extern "C" hipError_t rt_wf_bucket_sort(const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
-                                        uint32_t* vals_out, uint32_t n, uint32_t nb, int shift, uint32_t* cnt,
-                                        hipStream_t stream);
+                                        uint32_t* vals_out, uint32_t n, const uint32_t* n_dev, uint32_t nb, int shift,
+                                        uint32_t* cnt, hipStream_t stream);
 extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                                        const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit,
                                        hipStream_t stream);
 
 // Pair-path arrays (render_kernels.hip "wavefront pair path"): per ray of a level (R = the larger of
 // the pixel slots and the level capacity) and, grow-only, the pair lists for `need` pairs.
-static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t need, WfPairs* P) {
+static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t lcap, size_t need, WfPairs* P) {
   const size_t nl = (size_t)std::max(1, c->dev.n_lights);
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t o_omin = al(R * 8), o_px = al(o_omin + R * 4), o_k = al(o_px + 3 * R * 8), o_q = al(o_k + R * nl * 4);
@@ -2695,11 +2705,11 @@ static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t need, WfPairs* 
     c->wfr_bytes = rbytes;
   }
   if (need > c->wfp_cap || !c->wfp) {
-    const size_t cap = std::min<size_t>(0x7fffffc0ull, std::max<size_t>(need + need / 4, 8 * R) + 63) & ~(size_t)63;
+    // first size: 4 pairs per ray of a full level (fractal.scene needs ~3); a level that emits more
+    // grows it (RT_OPT_WAVEFRONT_CAP 1 % makes the first size tiny: the overflow tests take that path)
+    const size_t cap = std::min<size_t>(0x7fffffc0ull, std::max<size_t>(need + need / 4, 4 * lcap) + 63) & ~(size_t)63;
     if (need > cap) return fail(RT_ERR_UNSUPPORTED, "wavefront pair list of %zu pairs too large", need);
-    size_t sort_bytes = 0;
-    RT_HIP(rt_wf_sort_pairs(nullptr, &sort_bytes, nullptr, nullptr, nullptr, nullptr, (int)cap, 32, st));
-    const size_t bytes = al(256 + 16384 + 4 * cap * 4 + cap * 8) + sort_bytes + 256;
+    const size_t bytes = al(256 + 16384 + 4 * cap * 4 + cap * 8);
     if (c->wfp) (void)hipFree(c->wfp);    // waits for launches that may still use it
     c->wfp = nullptr;
     c->wfp_bytes = 0;
@@ -2735,63 +2745,50 @@ static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t need, WfPairs* 
 
 // One level of the wavefront path through the pair path: candidate pairs, sort by object, pair
 // evaluation and the folds, for the nearest hits and then the shadow rays, then the shading pass.
-// The host reads each pair count (a synchronisation): the sort and the evaluation grids are exact,
-// and a count beyond the arena grows it and re-runs the candidate pass.
+// The pair counts stay on the device (the sorts and the evaluation kernels read them; their grids
+// are sized for the arena), so a level costs ONE host synchronisation, at its end: it reads the next
+// level's ray count and both pair counts.  A pair count beyond the arena grows it and runs the level
+// again (the level's outputs are recomputed from its rays; level d + 1 is refilled from empty).
 static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int d, uint32_t n, int a0, int a1,
-                     int a2, int a3, int max_depth, bool refr, bool fc) {
+                     int a2, int a3, int max_depth, bool refr, bool fc, uint32_t* next) {
   WfPairs P;
-  int rc = wfp_arena(c, st, R, 0, &P);
+  int rc = wfp_arena(c, st, R, A.cap, 0, &P);
   if (rc) return rc;
-  int obits = 1;
-  while (obits < 32 && (1u << obits) < (uint32_t)c->dev.n_objects) ++obits;
   const dim3 g((n + 63) / 64), b64(64);
-  for (int pass = 0; pass < 2; ++pass) {
-    uint32_t np = 0;
-    if (pass == 1) {                  // the hit points and their order for the shadow and shading passes
-      hipLaunchKernelGGL(wfp_hit_key_kernel, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, c->dev,
-                         A, P, d, n, a0, a1, a2, a3);
-      size_t tb = c->wfp_bytes - (size_t)((uint8_t*)(P.tp + P.cap) - (uint8_t*)c->wfp) - 256;
-      void* tmp = (void*)(((uintptr_t)(P.tp + P.cap) + 255) & ~(uintptr_t)255);
-      // 4096 buckets of the key's top 12 bits (a 16^3 grid of hit-point cells), unordered within a
-      // bucket: 0.4 ms per fractal frame faster than the full 27-bit radix sort (rocPRIM's small-size
-      // path is a dozen merge launches), profiles/r03o_sort_ab.txt
-      RT_HIP(rt_wf_bucket_sort(P.hkey, P.hkey_s, P.hval, P.hperm, n, 4096, 15, P.bins, st));
-      (void)tb;
-      (void)tmp;
-    }
-    for (;;) {
-      RT_HIP(hipMemsetAsync(P.count, 0, 4, st));
-      if (pass == 0) hipLaunchKernelGGL((wfp_cand_kernel<false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
-      else hipLaunchKernelGGL((wfp_cand_kernel<true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
-      RT_HIP(hipGetLastError());
-      RT_HIP(hipMemcpyAsync(&np, P.count, 4, hipMemcpyDeviceToHost, st));
-      RT_HIP(hipStreamSynchronize(st));
-      if (np <= P.cap) break;
-      rc = wfp_arena(c, st, R, np, &P);
-      if (rc) return rc;
-    }
-    if (np == 0) continue;
-    size_t tb = c->wfp_bytes - (size_t)((uint8_t*)(P.tp + P.cap) - (uint8_t*)c->wfp) - 256;
-    void* tmp = (void*)(((uintptr_t)(P.tp + P.cap) + 255) & ~(uintptr_t)255);
-    if (c->dev.n_objects <= 4096)
-      RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, np, (uint32_t)c->dev.n_objects, 0, P.bins, st));
-    else
-      RT_HIP(rt_wf_sort_pairs(tmp, &tb, P.key, P.key_s, P.val, P.val_s, (int)np, obits, st));
-    const dim3 ge((np + 63) / 64);
-    if (pass == 0) {
-      hipLaunchKernelGGL(wfp_near_eval_kernel, ge, b64, 0, st, c->dev, A, P, d, np, a0, a1, a2, a3);
-      hipLaunchKernelGGL(wfp_near_tie_kernel, dim3(std::min<uint32_t>((np + 255) / 256, 4096)), dim3(256), 0, st, P, np);
-    } else {
-      hipLaunchKernelGGL(wfp_shadow_eval_kernel, ge, b64, 0, st, c->dev, P, np);
-    }
+  const uint32_t nobj = (uint32_t)c->dev.n_objects;
+  for (;;) {
+    const dim3 ge(std::min<uint32_t>((P.cap + 63) / 64, (uint32_t)c->n_cu * 32u));   // grid-stride evaluations
+    RT_HIP(hipMemsetAsync(P.count, 0, 8, st));
+    hipLaunchKernelGGL((wfp_cand_kernel<false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+    RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count, nobj, 0, P.bins, st));
+    hipLaunchKernelGGL(wfp_near_eval_kernel, ge, b64, 0, st, c->dev, A, P, d, a0, a1, a2, a3);
+    hipLaunchKernelGGL(wfp_near_tie_kernel, dim3(std::min<uint32_t>((P.cap + 255) / 256, 4096)), dim3(256), 0, st, P);
+    // the hit points and their order for the shadow and shading passes: at most 4096 buckets of
+    // (hit object, coarse hit-point cell), unordered within a bucket (a 16^3-cell-only key and the
+    // full 27-bit radix sort measured slower: profiles/r03o_sort_ab.txt, r03w_*)
+    int cbits = 0;
+    while (cbits < 12 && ((nobj + 1u) << (cbits + 1)) <= 4096u) ++cbits;
+    hipLaunchKernelGGL(wfp_hit_key_kernel, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, c->dev,
+                       A, P, d, n, a0, a1, a2, a3, cbits);
+    RT_HIP(rt_wf_bucket_sort(P.hkey, P.hkey_s, P.hval, P.hperm, n, nullptr, (nobj + 1u) << cbits, 0, P.bins, st));
+    hipLaunchKernelGGL((wfp_cand_kernel<true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+    RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count + 1, nobj, 0, P.bins, st));
+    hipLaunchKernelGGL(wfp_shadow_eval_kernel, ge, b64, 0, st, c->dev, P);
+    if (refr && fc) hipLaunchKernelGGL((wfp_shade_kernel<true, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
+    else if (refr) hipLaunchKernelGGL((wfp_shade_kernel<true, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
+    else if (fc) hipLaunchKernelGGL((wfp_shade_kernel<false, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
+    else hipLaunchKernelGGL((wfp_shade_kernel<false, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
     RT_HIP(hipGetLastError());
+    uint32_t pc[2] = {0, 0};
+    *next = 0;
+    RT_HIP(hipMemcpyAsync(pc, P.count, 8, hipMemcpyDeviceToHost, st));
+    if (d < max_depth) RT_HIP(hipMemcpyAsync(next, A.count + d + 1, 4, hipMemcpyDeviceToHost, st));
+    RT_HIP(hipStreamSynchronize(st));
+    if (pc[0] <= P.cap && pc[1] <= P.cap) return RT_OK;
+    rc = wfp_arena(c, st, R, A.cap, std::max(pc[0], pc[1]), &P);   // grow (synchronises), then this level again
+    if (rc) return rc;
+    if (d < max_depth) RT_HIP(hipMemsetAsync(A.count + d + 1, 0, 4, st));
   }
-  if (refr && fc) hipLaunchKernelGGL((wfp_shade_kernel<true, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
-  else if (refr) hipLaunchKernelGGL((wfp_shade_kernel<true, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
-  else if (fc) hipLaunchKernelGGL((wfp_shade_kernel<false, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
-  else hipLaunchKernelGGL((wfp_shade_kernel<false, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
-  RT_HIP(hipGetLastError());
-  return RT_OK;
 }
 
 // The wavefront path (wf_*_kernel): level 0 (the pixel slots), then each level the previous one
@@ -2832,7 +2829,7 @@ static int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, i
   RT_HIP(hipMemsetAsync(A.count, 0, 256, st));
   RT_HIP(hipMemsetAsync(A.ovf, 0, slots, st));
   const bool refr = c->dev.any_transparent != 0, fc = c->dev.colour_fast != 0 && c->fast_clamp;
-  const bool pairs = c->wf_pairs > 0 && c->dev.shadow_pow != 0 && c->dev.n_objects > 0;
+  const bool pairs = c->wf_pairs > 0 && c->dev.shadow_pow != 0 && c->dev.n_objects > 0 && c->dev.n_objects <= 4096;
   auto pairs_level = [&](int d) { return pairs && (d > 0 || c->wf_pairs == 2); };
   uint32_t n_level[RT_MAX_DEPTH_CAP + 2] = {0};
   n_level[0] = (uint32_t)slots;
@@ -2855,8 +2852,11 @@ static int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, i
     }
     const dim3 g((n + 63) / 64);
     if (pairs_level(d)) {
-      int rc = wfp_level(c, st, A, std::max(slots, cap), d, n, a0, a1, a2, a3, max_depth, refr, fc);
+      uint32_t cnt = 0;
+      int rc = wfp_level(c, st, A, std::max(slots, cap), d, n, a0, a1, a2, a3, max_depth, refr, fc, &cnt);
       if (rc) return rc;
+      if (d < max_depth) n_level[d + 1] = std::min<uint32_t>(cnt, (uint32_t)cap);
+      continue;
     }
     else if (refr && fc) hipLaunchKernelGGL((wf_trace_kernel<true, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
     else if (refr) hipLaunchKernelGGL((wf_trace_kernel<true, false>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);

@@ -30,8 +30,11 @@ extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const u
 __device__ __forceinline__ uint32_t rt_bs_bin(uint32_t key, int shift, uint32_t nb) {
   return min(key >> shift, nb - 1u);
 }
-__global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t nb,
-                                                           int shift, uint32_t* __restrict__ cnt) {
+// n_dev != nullptr: the item count is min(*n_dev, n) (a count another kernel wrote: no host read)
+__global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_hist(const uint32_t* __restrict__ keys, uint32_t n,
+                                                           const uint32_t* __restrict__ n_dev, uint32_t nb, int shift,
+                                                           uint32_t* __restrict__ cnt) {
+  if (n_dev) n = min(*n_dev, n);
   __shared__ uint32_t h[RT_BS_MAX_BINS];
   for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
   __syncthreads();
@@ -65,48 +68,55 @@ __global__ __launch_bounds__(1024) void rt_bs_scan(uint32_t* __restrict__ cnt, u
 
 __global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_scatter(const uint32_t* __restrict__ keys,
                                                               const uint32_t* __restrict__ vals, uint32_t n,
-                                                              uint32_t nb, int shift, uint32_t* __restrict__ off,
+                                                              const uint32_t* __restrict__ n_dev, uint32_t nb,
+                                                              int shift, uint32_t* __restrict__ off,
                                                               uint32_t* __restrict__ keys_out,
                                                               uint32_t* __restrict__ vals_out) {
+  if (n_dev) n = min(*n_dev, n);
   __shared__ uint32_t h[RT_BS_MAX_BINS];
-  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
-  __syncthreads();
-  const uint32_t base = blockIdx.x * (RT_BS_THREADS * RT_BS_PER_THREAD);
-  uint32_t k[RT_BS_PER_THREAD], r[RT_BS_PER_THREAD];
+  constexpr uint32_t CH = RT_BS_THREADS * RT_BS_PER_THREAD;
+  for (uint32_t base = blockIdx.x * CH; base < n; base += gridDim.x * CH) {   // chunks, grid-stride
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+    uint32_t k[RT_BS_PER_THREAD], r[RT_BS_PER_THREAD];
 #pragma unroll
-  for (int e = 0; e < RT_BS_PER_THREAD; ++e) {
-    const uint32_t i = base + (uint32_t)e * RT_BS_THREADS + threadIdx.x;
-    k[e] = i < n ? rt_bs_bin(keys[i], shift, nb) : 0u;
-    r[e] = i < n ? atomicAdd(&h[k[e]], 1u) : 0u;
-  }
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
-    if (h[b]) h[b] = atomicAdd(&off[b], h[b]);              // this chunk's run in bucket b
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < RT_BS_PER_THREAD; ++e) {
-    const uint32_t i = base + (uint32_t)e * RT_BS_THREADS + threadIdx.x;
-    if (i < n) {
-      const uint32_t q = h[k[e]] + r[e];
-      keys_out[q] = k[e];
-      vals_out[q] = vals[i];
+    for (int e = 0; e < RT_BS_PER_THREAD; ++e) {
+      const uint32_t i = base + (uint32_t)e * RT_BS_THREADS + threadIdx.x;
+      k[e] = i < n ? rt_bs_bin(keys[i], shift, nb) : 0u;
+      r[e] = i < n ? atomicAdd(&h[k[e]], 1u) : 0u;
     }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+      if (h[b]) h[b] = atomicAdd(&off[b], h[b]);            // this chunk's run in bucket b
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < RT_BS_PER_THREAD; ++e) {
+      const uint32_t i = base + (uint32_t)e * RT_BS_THREADS + threadIdx.x;
+      if (i < n) {
+        const uint32_t q = h[k[e]] + r[e];
+        keys_out[q] = k[e];
+        vals_out[q] = vals[i];
+      }
+    }
+    __syncthreads();
   }
 }
 
 // Sorts n (key, value) pairs by bin = min(key >> shift, nb - 1) (nb <= RT_BS_MAX_BINS) into keys_out
-// (the bins) / vals_out; cnt: nb words of device scratch.
+// (the bins) / vals_out; cnt: nb words of device scratch.  n_dev != nullptr: the count is
+// min(*n_dev, n), read on the device (n is then the capacity the grids are sized for).
 extern "C" hipError_t rt_wf_bucket_sort(const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
-                                        uint32_t* vals_out, uint32_t n, uint32_t nb, int shift, uint32_t* cnt,
-                                        hipStream_t stream) {
+                                        uint32_t* vals_out, uint32_t n, const uint32_t* n_dev, uint32_t nb, int shift,
+                                        uint32_t* cnt, hipStream_t stream) {
   if (nb == 0 || nb > RT_BS_MAX_BINS) return hipErrorInvalidValue;
   if (n == 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nb * 4, stream);
   if (e != hipSuccess) return e;
-  const uint32_t chunk = RT_BS_THREADS * RT_BS_PER_THREAD, gh = std::min<uint32_t>((n + chunk - 1) / chunk, 2048u);
-  hipLaunchKernelGGL(rt_bs_hist, dim3(gh), dim3(RT_BS_THREADS), 0, stream, keys_in, n, nb, shift, cnt);
+  const uint32_t chunk = RT_BS_THREADS * RT_BS_PER_THREAD, gc = (n + chunk - 1) / chunk;
+  hipLaunchKernelGGL(rt_bs_hist, dim3(std::min<uint32_t>(gc, 1024u)), dim3(RT_BS_THREADS), 0, stream, keys_in, n, n_dev,
+                     nb, shift, cnt);
   hipLaunchKernelGGL(rt_bs_scan, dim3(1), dim3(1024), 0, stream, cnt, nb);
-  hipLaunchKernelGGL(rt_bs_scatter, dim3((n + chunk - 1) / chunk), dim3(RT_BS_THREADS), 0, stream, keys_in, vals_in, n,
-                     nb, shift, cnt, keys_out, vals_out);
+  hipLaunchKernelGGL(rt_bs_scatter, dim3(std::min<uint32_t>(gc, 2048u)), dim3(RT_BS_THREADS), 0, stream, keys_in,
+                     vals_in, n, n_dev, nb, shift, cnt, keys_out, vals_out);
   return hipGetLastError();
 }
