@@ -1773,6 +1773,8 @@ struct WfPairs {
 #define RT_WFP_BUF 512          // pairs buffered in LDS per wave before one atomic allocates their slots
 #endif
 constexpr unsigned long long RT_WFP_NONE = 0x7FF0000000000000ull;   // +inf
+constexpr int RT_WFP_COUNT = 32;      // the pair counts' words in WfArena::count (after the level counts)
+static_assert(RT_MAX_DEPTH_CAP + 3 <= RT_WFP_COUNT, "wavefront counter block");
 
 // Ray of slot j of level d (level 0: the pixel slot's camera ray).
 __device__ __forceinline__ bool wf_get_ray(const RtDevScene& S, const WfLevel& lv, int d, uint32_t j, int y_first,
@@ -2685,7 +2687,7 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
 
 extern "C" hipError_t rt_wf_bucket_sort(const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
                                         uint32_t* vals_out, uint32_t n, const uint32_t* n_dev, uint32_t nb, int shift,
-                                        uint32_t* cnt, hipStream_t stream);
+                                        uint32_t* cnt, bool zero_cnt, hipStream_t stream);
 extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                                        const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit,
                                        hipStream_t stream);
@@ -2709,7 +2711,7 @@ static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t lcap, size_t ne
     // grows it (RT_OPT_WAVEFRONT_CAP 1 % makes the first size tiny: the overflow tests take that path)
     const size_t cap = std::min<size_t>(0x7fffffc0ull, std::max<size_t>(need + need / 4, 4 * lcap) + 63) & ~(size_t)63;
     if (need > cap) return fail(RT_ERR_UNSUPPORTED, "wavefront pair list of %zu pairs too large", need);
-    const size_t bytes = al(256 + 16384 + 4 * cap * 4 + cap * 8);
+    const size_t bytes = al(3 * 16384 + 4 * cap * 4 + cap * 8);
     if (c->wfp) (void)hipFree(c->wfp);    // waits for launches that may still use it
     c->wfp = nullptr;
     c->wfp_bytes = 0;
@@ -2733,9 +2735,9 @@ static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t lcap, size_t ne
   uint8_t* b = (uint8_t*)c->wfp;
   const size_t cap = c->wfp_cap;
   P->cap = (uint32_t)cap;
-  P->count = (uint32_t*)b;
-  P->bins = (uint32_t*)(b + 256);
-  P->key = (uint32_t*)(b + 256 + 16384);
+  P->count = nullptr;                   // set by the caller: the wavefront arena's counter block
+  P->bins = (uint32_t*)b;               // 3 x RT_BS_MAX_BINS words: nearest / hit-point / shadow sorts
+  P->key = (uint32_t*)(b + 3 * 16384);
   P->val = P->key + cap;
   P->key_s = P->val + cap;
   P->val_s = P->key_s + cap;
@@ -2754,13 +2756,16 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
   WfPairs P;
   int rc = wfp_arena(c, st, R, A.cap, 0, &P);
   if (rc) return rc;
+  P.count = A.count + RT_WFP_COUNT;
   const dim3 g((n + 63) / 64), b64(64);
   const uint32_t nobj = (uint32_t)c->dev.n_objects;
+  uint32_t* bins[3] = {P.bins, P.bins + 4096, P.bins + 8192};
   for (;;) {
     const dim3 ge(std::min<uint32_t>((P.cap + 63) / 64, (uint32_t)c->n_cu * 32u));   // grid-stride evaluations
     RT_HIP(hipMemsetAsync(P.count, 0, 8, st));
+    RT_HIP(hipMemsetAsync(P.bins, 0, 3 * 16384, st));        // the three sorts' bucket counters
     hipLaunchKernelGGL((wfp_cand_kernel<false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
-    RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count, nobj, 0, P.bins, st));
+    RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count, nobj, 0, bins[0], false, st));
     hipLaunchKernelGGL(wfp_near_eval_kernel, ge, b64, 0, st, c->dev, A, P, d, a0, a1, a2, a3);
     hipLaunchKernelGGL(wfp_near_tie_kernel, dim3(std::min<uint32_t>((P.cap + 255) / 256, 4096)), dim3(256), 0, st, P);
     // the hit points and their order for the shadow and shading passes: at most 4096 buckets of
@@ -2770,23 +2775,25 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
     while (cbits < 12 && ((nobj + 1u) << (cbits + 1)) <= 4096u) ++cbits;
     hipLaunchKernelGGL(wfp_hit_key_kernel, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, c->dev,
                        A, P, d, n, a0, a1, a2, a3, cbits);
-    RT_HIP(rt_wf_bucket_sort(P.hkey, P.hkey_s, P.hval, P.hperm, n, nullptr, (nobj + 1u) << cbits, 0, P.bins, st));
+    RT_HIP(rt_wf_bucket_sort(P.hkey, P.hkey_s, P.hval, P.hperm, n, nullptr, (nobj + 1u) << cbits, 0, bins[1], false, st));
     hipLaunchKernelGGL((wfp_cand_kernel<true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
-    RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count + 1, nobj, 0, P.bins, st));
+    RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count + 1, nobj, 0, bins[2], false, st));
     hipLaunchKernelGGL(wfp_shadow_eval_kernel, ge, b64, 0, st, c->dev, P);
     if (refr && fc) hipLaunchKernelGGL((wfp_shade_kernel<true, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
     else if (refr) hipLaunchKernelGGL((wfp_shade_kernel<true, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
     else if (fc) hipLaunchKernelGGL((wfp_shade_kernel<false, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
     else hipLaunchKernelGGL((wfp_shade_kernel<false, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
     RT_HIP(hipGetLastError());
-    uint32_t pc[2] = {0, 0};
-    *next = 0;
-    RT_HIP(hipMemcpyAsync(pc, P.count, 8, hipMemcpyDeviceToHost, st));
-    if (d < max_depth) RT_HIP(hipMemcpyAsync(next, A.count + d + 1, 4, hipMemcpyDeviceToHost, st));
+    uint32_t cb[RT_WFP_COUNT + 2];        // the whole counter block in one copy: level counts, pair counts
+    RT_HIP(hipMemcpyAsync(cb, A.count, sizeof cb, hipMemcpyDeviceToHost, st));
     RT_HIP(hipStreamSynchronize(st));
+    *next = d < max_depth ? cb[d + 1] : 0u;
+    const uint32_t pc[2] = {cb[RT_WFP_COUNT], cb[RT_WFP_COUNT + 1]};
     if (pc[0] <= P.cap && pc[1] <= P.cap) return RT_OK;
     rc = wfp_arena(c, st, R, A.cap, std::max(pc[0], pc[1]), &P);   // grow (synchronises), then this level again
     if (rc) return rc;
+    P.count = A.count + RT_WFP_COUNT;
+    bins[0] = P.bins; bins[1] = P.bins + 4096; bins[2] = P.bins + 8192;
     if (d < max_depth) RT_HIP(hipMemsetAsync(A.count + d + 1, 0, 4, st));
   }
 }

@@ -104,14 +104,17 @@ __global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_scatter(const uint32_t* _
 
 // Sorts n (key, value) pairs by bin = min(key >> shift, nb - 1) (nb <= RT_BS_MAX_BINS) into keys_out
 // (the bins) / vals_out; cnt: nb words of device scratch.  n_dev != nullptr: the count is
-// min(*n_dev, n), read on the device (n is then the capacity the grids are sized for).
+// min(*n_dev, n), read on the device (n is then the capacity the grids are sized for).  zero_cnt =
+// false: the caller already zeroed cnt[0, nb) on this stream.
 extern "C" hipError_t rt_wf_bucket_sort(const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
                                         uint32_t* vals_out, uint32_t n, const uint32_t* n_dev, uint32_t nb, int shift,
-                                        uint32_t* cnt, hipStream_t stream) {
+                                        uint32_t* cnt, bool zero_cnt, hipStream_t stream) {
   if (nb == 0 || nb > RT_BS_MAX_BINS) return hipErrorInvalidValue;
   if (n == 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nb * 4, stream);
-  if (e != hipSuccess) return e;
+  if (zero_cnt) {
+    hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nb * 4, stream);
+    if (e != hipSuccess) return e;
+  }
   const uint32_t chunk = RT_BS_THREADS * RT_BS_PER_THREAD, gc = (n + chunk - 1) / chunk;
   hipLaunchKernelGGL(rt_bs_hist, dim3(std::min<uint32_t>(gc, 1024u)), dim3(RT_BS_THREADS), 0, stream, keys_in, n, n_dev,
                      nb, shift, cnt);
