@@ -1463,8 +1463,9 @@ struct WfLevel {
   double *Lr, *Lg, *Lb, *wt, *wr;        // hit record: L (then the folded colour), refraction / reflection weights
   int32_t *pix, *ct, *cr;                // pixel slot (levels >= 1), children's slots in level d + 1 (-1: none)
   uint32_t *key, *val;                   // levels >= 1: coherence key and slot (the sort's input pairs)
+  int32_t* par;                          // levels >= 1: the object whose hit spawned the ray
 };
-constexpr size_t RT_WF_BYTES0 = 5 * 8 + 2 * 4, RT_WF_BYTES = 11 * 8 + 5 * 4;
+constexpr size_t RT_WF_BYTES0 = 5 * 8 + 2 * 4, RT_WF_BYTES = 11 * 8 + 6 * 4;
 __host__ __device__ __forceinline__ WfLevel wf_level(const WfArena& A, int d) {
   WfLevel v;
   const size_t len = d == 0 ? A.slots : A.cap;
@@ -1475,12 +1476,14 @@ __host__ __device__ __forceinline__ WfLevel wf_level(const WfArena& A, int d) {
     int32_t* q = (int32_t*)(f + 5 * len);
     v.pix = nullptr; v.ct = q; v.cr = q + len;
     v.key = v.val = nullptr;
+    v.par = nullptr;
   } else {
     v.ox = f; v.oy = f + len; v.oz = f + 2 * len; v.dx = f + 3 * len; v.dy = f + 4 * len; v.dz = f + 5 * len;
     v.Lr = f + 6 * len; v.Lg = f + 7 * len; v.Lb = f + 8 * len; v.wt = f + 9 * len; v.wr = f + 10 * len;
     int32_t* q = (int32_t*)(f + 11 * len);
     v.pix = q; v.ct = q + len; v.cr = q + 2 * len;
     v.key = (uint32_t*)(q + 3 * len); v.val = (uint32_t*)(q + 4 * len);
+    v.par = q + 5 * len;
   }
   return v;
 }
@@ -1596,7 +1599,7 @@ __device__ __forceinline__ void wf_ray(const DS& S, V3 ro, V3 rd, int depth, int
 // record at the ray's slot j.
 __device__ __forceinline__ void wf_append(const WfArena& A, const WfLevel& lv, int d, int lane, bool live, uint32_t j,
                                           int32_t pix, Col L, double wt, double wr, bool ch_t, bool ch_r, V3 p, V3 dt,
-                                          V3 dr) {
+                                          V3 dr, int32_t par = -1) {
   int32_t ct = -1, cr = -1;
   const uint64_t bt = __ballot(ch_t), br = __ballot(ch_r);
   const uint32_t nt = (uint32_t)__popcll(bt), nr = (uint32_t)__popcll(br);
@@ -1611,14 +1614,14 @@ __device__ __forceinline__ void wf_append(const WfArena& A, const WfLevel& lv, i
     if (ch_t) {
       if (st < A.cap) {
         nx.ox[st] = p.x; nx.oy[st] = p.y; nx.oz[st] = p.z; nx.dx[st] = dt.x; nx.dy[st] = dt.y; nx.dz[st] = dt.z;
-        nx.pix[st] = pix; nx.key[st] = wf_key(A, p, dt); nx.val[st] = st;
+        nx.pix[st] = pix; nx.key[st] = wf_key(A, p, dt); nx.val[st] = st; nx.par[st] = par;
         ct = (int32_t)st;
       } else ovf = true;
     }
     if (ch_r) {
       if (sr < A.cap) {
         nx.ox[sr] = p.x; nx.oy[sr] = p.y; nx.oz[sr] = p.z; nx.dx[sr] = dr.x; nx.dy[sr] = dr.y; nx.dz[sr] = dr.z;
-        nx.pix[sr] = pix; nx.key[sr] = wf_key(A, p, dr); nx.val[sr] = sr;
+        nx.pix[sr] = pix; nx.key[sr] = wf_key(A, p, dr); nx.val[sr] = sr; nx.par[sr] = par;
         cr = (int32_t)sr;
       } else ovf = true;
     }
@@ -1776,6 +1779,60 @@ constexpr unsigned long long RT_WFP_NONE = 0x7FF0000000000000ull;   // +inf
 constexpr int RT_WFP_COUNT = 32;      // the pair counts' words in WfArena::count (after the level counts)
 static_assert(RT_MAX_DEPTH_CAP + 3 <= RT_WFP_COUNT, "wavefront counter block");
 
+// The object's nearest accepted distance for one ray: nearest_hit's body for one object, its best
+// starting at +inf (the leaf boxes' tmax only shrinks, as share_prev requires).
+__device__ __forceinline__ double wfp_object_nearest(const DS& S, int o, V3 ro, V3 rd, const CullRay& cr) {
+  cptr<RtObject> O = &S.objects[o];
+  const bool fin = wave_finite(ro, rd);
+  double best = INFINITY;
+  SphereShare shr = {0.0, 0.0, 0.0};
+  const int lb = O->leaf_begin, le = lb + O->leaf_count;
+  for (int l = lb; l < le; ++l) {
+    cptr<RtLeaf> L = &S.leaves[l];
+    if (O->leaf_cull) {
+      if (L->cull == RT_CULL_ALWAYS) continue;
+      if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, cull_tmax(best))) continue;
+    }
+    double t0 = 0.0, t1 = 0.0;
+    const int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1, RT_SPHERE_SHARE ? &shr : nullptr);
+    const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && L->filter_const && !isnan(cr.inv.x));
+    if (n >= 1 && t0 > EPS && t0 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) best = t0;
+    if (n >= 2 && t1 > EPS && t1 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t1))))) best = t1;
+  }
+  return best;
+}
+
+// Filtered hits of the object with EPS < t < dist on one shadow ray (shadow_transparency's body for
+// one object); a zero-transparency object stops at its first.
+__device__ __forceinline__ uint32_t wfp_object_shadow(const DS& S, int o, V3 p, V3 dir, double dist, const CullRay& cr) {
+  cptr<RtObject> O = &S.objects[o];
+  const bool fin = wave_finite(p, dir);
+  const double tmax = cull_tmax(dist);
+  const bool zero = O->transparency == 0.0;
+  uint32_t cnt = 0;
+  SphereShare shr = {0.0, 0.0, 0.0};
+  const int lb = O->leaf_begin, le = lb + O->leaf_count;
+  for (int l = lb; l < le; ++l) {
+    cptr<RtLeaf> L = &S.leaves[l];
+    if (O->leaf_cull) {
+      if (L->cull == RT_CULL_ALWAYS) continue;
+      if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
+    }
+    double t0 = 0.0, t1 = 0.0;
+    const int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1, RT_SPHERE_SHARE ? &shr : nullptr);
+    const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && L->filter_const && !isnan(cr.inv.x));
+    if (n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) {
+      ++cnt;
+      if (zero) return cnt;
+    }
+    if (n >= 2 && t1 > EPS && t1 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t1))))) {
+      ++cnt;
+      if (zero) return cnt;
+    }
+  }
+  return cnt;
+}
+
 // Ray of slot j of level d (level 0: the pixel slot's camera ray).
 __device__ __forceinline__ bool wf_get_ray(const RtDevScene& S, const WfLevel& lv, int d, uint32_t j, int y_first,
                                            int band_rows, int band_pitch, int n_rows, V3* ro, V3* rd) {
@@ -1858,7 +1915,23 @@ __global__ __launch_bounds__(64) void wfp_cand_kernel(RtDevScene S, WfArena A, W
   };
   if constexpr (!SHADOW) {
     if (i < n) { P.tmin[j] = RT_WFP_NONE; P.omin[j] = 0x7fffffff; }   // slots outside the frame too
-    walk(live, ro, rd, INFINITY, j);
+    // A bound on the nearest hit: the object whose hit spawned the ray, evaluated first (a ray that
+    // refracted into or reflects inside a closed shape meets it again).  The walk then tests boxes
+    // against [0, cull_tmax(bound)] only -- conservative, as nearest_hit's running best is; the
+    // parent's own pair is still emitted by the walk (its box contains the bound's point).
+    double bound = INFINITY;
+    if (d > 0) {
+      const int32_t par = live ? lv.par[j] : -1;
+      const CullRay cr = cull_ray(ro, rd);
+      uint64_t todo = __ballot(live && par >= 0);
+      while (todo) {                     // the children of one shading wave: mostly one parent
+        const int pu = __builtin_amdgcn_readlane(par, (int)__builtin_ctzll(todo));
+        const uint64_t mine = __ballot(live && par == pu);
+        todo &= ~mine;
+        if ((mine >> lane) & 1) bound = wfp_object_nearest(D, pu, ro, rd, cr);
+      }
+    }
+    walk(live, ro, rd, bound < INFINITY ? cull_tmax(bound) : INFINITY, j);
   } else {
     const int32_t oi = live ? P.omin[j] : 0x7fffffff;
     const bool hit = live && oi != 0x7fffffff;
@@ -1882,60 +1955,6 @@ __global__ __launch_bounds__(64) void wfp_cand_kernel(RtDevScene S, WfArena A, W
     }
   }
   flush();
-}
-
-// The object's nearest accepted distance for one ray: nearest_hit's body for one object, its best
-// starting at +inf (the leaf boxes' tmax only shrinks, as share_prev requires).
-__device__ __forceinline__ double wfp_object_nearest(const DS& S, int o, V3 ro, V3 rd, const CullRay& cr) {
-  cptr<RtObject> O = &S.objects[o];
-  const bool fin = wave_finite(ro, rd);
-  double best = INFINITY;
-  SphereShare shr = {0.0, 0.0, 0.0};
-  const int lb = O->leaf_begin, le = lb + O->leaf_count;
-  for (int l = lb; l < le; ++l) {
-    cptr<RtLeaf> L = &S.leaves[l];
-    if (O->leaf_cull) {
-      if (L->cull == RT_CULL_ALWAYS) continue;
-      if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, cull_tmax(best))) continue;
-    }
-    double t0 = 0.0, t1 = 0.0;
-    const int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1, RT_SPHERE_SHARE ? &shr : nullptr);
-    const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && L->filter_const && !isnan(cr.inv.x));
-    if (n >= 1 && t0 > EPS && t0 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) best = t0;
-    if (n >= 2 && t1 > EPS && t1 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t1))))) best = t1;
-  }
-  return best;
-}
-
-// Filtered hits of the object with EPS < t < dist on one shadow ray (shadow_transparency's body for
-// one object); a zero-transparency object stops at its first.
-__device__ __forceinline__ uint32_t wfp_object_shadow(const DS& S, int o, V3 p, V3 dir, double dist, const CullRay& cr) {
-  cptr<RtObject> O = &S.objects[o];
-  const bool fin = wave_finite(p, dir);
-  const double tmax = cull_tmax(dist);
-  const bool zero = O->transparency == 0.0;
-  uint32_t cnt = 0;
-  SphereShare shr = {0.0, 0.0, 0.0};
-  const int lb = O->leaf_begin, le = lb + O->leaf_count;
-  for (int l = lb; l < le; ++l) {
-    cptr<RtLeaf> L = &S.leaves[l];
-    if (O->leaf_cull) {
-      if (L->cull == RT_CULL_ALWAYS) continue;
-      if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
-    }
-    double t0 = 0.0, t1 = 0.0;
-    const int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1, RT_SPHERE_SHARE ? &shr : nullptr);
-    const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && L->filter_const && !isnan(cr.inv.x));
-    if (n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) {
-      ++cnt;
-      if (zero) return cnt;
-    }
-    if (n >= 2 && t1 > EPS && t1 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t1))))) {
-      ++cnt;
-      if (zero) return cnt;
-    }
-  }
-  return cnt;
 }
 
 // One lane per sorted pair: the waves see one object (two at a run boundary): scalarised over the
@@ -2084,7 +2103,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER
           return tr;
         },
         &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr);
-  wf_append(A, lv, d, lane, live, j, pix, L, wt, wr, ch_t, ch_r, p, dt, dr);
+  wf_append(A, lv, d, lane, live, j, pix, L, wt, wr, ch_t, ch_r, p, dt, dr, live ? P.omin[j] : -1);
 }
 
 template <bool REFR>
