@@ -21,13 +21,15 @@ if [ "${CONFIGS:-0}" = "1" ]; then
     cat $O/${T}_bench_$C.json
   done
 fi
-if [ "${KT:-1}" = "1" ]; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/${T}_bench_kt.json 2> $O/${T}_kt.err || { tail $O/${T}_kt.err; exit 1; }
-fi
 if [ "${PMC:-0}" = "1" ]; then
   for PMC in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64" "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES" "SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT"; do
     N=$(echo $PMC | tr ' ' '_' | cut -c1-40)
     timeout -s KILL 120 rocprofv3 --pmc $PMC --output-format csv -d $O/${T}_pmc_$N -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extra ${PMC_ARGS:-} > /dev/null 2> $O/${T}_pmc_$N.err || { echo "pmc pass $PMC failed (see $O/${T}_pmc_$N.err)"; exit 1; }
   done
+fi
+# last: rocprofv3 --kernel-trace over bench.py has segfaulted in __cxa_finalize after writing its
+# output (profiler teardown, no GPU fault), so nothing GPU-side follows it
+if [ "${KT:-1}" = "1" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra > $O/${T}_bench_kt.json 2> $O/${T}_kt.err || { tail $O/${T}_kt.err; exit 1; }
 fi
 echo session done
