@@ -37,7 +37,8 @@ def main():
         for n in (int(v) for v in a.ns.split(",")):
             band = 8
             n_bands = len(range(0, -(-H // band), n))
-            outs = [torch.empty((n_bands * band, W, 4), dtype=torch.uint8, device="cuda") for _ in range(4)]
+            kmax = max(int(v) for v in a.ks.split(","))
+            outs = [torch.empty((n_bands * band, W, 4), dtype=torch.uint8, device="cuda") for _ in range(max(4, kmax))]
             for k in (int(v) for v in a.ks.split(",")):
                 sys.path.insert(0, ROOT)
                 import tinyraytracerinrust_amd as T
