@@ -261,7 +261,7 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  * RT_OPT_WAVEFRONT_PAIRS: how the wavefront path traces a level's rays: 0 one wave walks the object
  * hierarchy for 64 rays (wf_trace_kernel); 1 (default) levels >= 1 go through (ray, object) pairs
  * sorted by object, so a wave tests one object against 64 rays (wfp_* kernels; scenes whose shadow
- * products are order-free, RtDevScene::shadow_pow, and at most 4096 objects; else as 0); 2 level 0
+ * products are order-free, RtDevScene::shadow_pow, and fewer than 4096 objects; else as 0); 2 level 0
  * (the camera rays) too. */
 typedef enum rt_option {
   RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4,

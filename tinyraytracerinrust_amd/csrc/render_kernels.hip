@@ -1586,10 +1586,11 @@ __device__ __forceinline__ void wf_ray_core(const DS& S, V3 ro, V3 rd, int depth
 
 template <bool REFR, bool FC>
 __device__ __forceinline__ void wf_ray(const DS& S, V3 ro, V3 rd, int depth, int max_depth, Col* Lo, double* wt,
-                                       double* wr, bool* ch_t, bool* ch_r, V3* po, V3* dt, V3* dr) {
+                                       double* wr, bool* ch_t, bool* ch_r, V3* po, V3* dt, V3* dr, int* hit_obj) {
   constexpr bool SHARE = REFR && RT_SPHERE_SHARE, OBB = !REFR;
   wf_ray_core<REFR, FC>(
-      S, ro, rd, depth, max_depth, [&](double* t) { return nearest_hit<SHARE, OBB>(S, ro, rd, t, depth == 0 ? 0 : 1); },
+      S, ro, rd, depth, max_depth,
+      [&](double* t) { return *hit_obj = nearest_hit<SHARE, OBB>(S, ro, rd, t, depth == 0 ? 0 : 1); },
       [&](int, V3 p, V3 sdir, double ll) { return shadow_transparency<SHARE, OBB>(S, p, sdir, ll); }, Lo, wt, wr, ch_t,
       ch_r, po, dt, dr);
 }
@@ -1665,8 +1666,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER
   double wt = 0.0, wr = 0.0;
   bool ch_t = false, ch_r = false;
   V3 p = {0.0, 0.0, 0.0}, dt = {0.0, 0.0, 0.0}, dr = {0.0, 0.0, 0.0};
-  if (live) wf_ray<REFR, FC>(make_ds(S), ro, rd, d, max_depth, &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr);
-  wf_append(A, lv, d, lane, live, j, pix, L, wt, wr, ch_t, ch_r, p, dt, dr);
+  int oi = -1;
+  if (live) wf_ray<REFR, FC>(make_ds(S), ro, rd, d, max_depth, &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr, &oi);
+  wf_append(A, lv, d, lane, live, j, pix, L, wt, wr, ch_t, ch_r, p, dt, dr, oi);
 }
 
 template <bool F64, bool FC>
@@ -2855,7 +2857,7 @@ static int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, i
   RT_HIP(hipMemsetAsync(A.count, 0, 256, st));
   RT_HIP(hipMemsetAsync(A.ovf, 0, slots, st));
   const bool refr = c->dev.any_transparent != 0, fc = c->dev.colour_fast != 0 && c->fast_clamp;
-  const bool pairs = c->wf_pairs > 0 && c->dev.shadow_pow != 0 && c->dev.n_objects > 0 && c->dev.n_objects <= 4096;
+  const bool pairs = c->wf_pairs > 0 && c->dev.shadow_pow != 0 && c->dev.n_objects > 0 && c->dev.n_objects < 4096;
   auto pairs_level = [&](int d) { return pairs && (d > 0 || c->wf_pairs == 2); };
   uint32_t n_level[RT_MAX_DEPTH_CAP + 2] = {0};
   n_level[0] = (uint32_t)slots;
