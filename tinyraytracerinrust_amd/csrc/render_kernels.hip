@@ -550,11 +550,13 @@ __device__ int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist, int cat = 0)
     }
     ++i;
     if (!act) continue;
+    // the object's cull kind and box come from the node's copy (RtTrav): one scalar load for the
+    // node decides the common case; the object's own record is read only once its box passes
+    if (T->cull == RT_CULL_ALWAYS) continue;
+    if (T->cull == RT_CULL_BOX) CNT(cb + 1);
+    if (T->cull == RT_CULL_BOX && !box_may_hit(T->blo, T->bhi, cr, cull_tmax(best))) continue;
     const int o = T->obj;
     cptr<RtObject> O = &S.objects[o];
-    if (O->cull == RT_CULL_ALWAYS) continue;
-    if (O->cull == RT_CULL_BOX) CNT(cb + 1);
-    if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, cr, cull_tmax(best))) continue;
     if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, ro, rd, cull_tmax(best))) continue;
     CNT(cb + 2);
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
@@ -618,10 +620,10 @@ __device__ double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
     }
     ++i;
     if (!act) continue;
+    if (T->shadow_skip || T->cull == RT_CULL_ALWAYS) continue;     // the node's copies (see nearest_hit)
+    if (T->cull == RT_CULL_BOX) CNT(cb + 1);
+    if (T->cull == RT_CULL_BOX && !box_may_hit(T->blo, T->bhi, cr, tmax)) continue;
     cptr<RtObject> O = &S.objects[T->obj];
-    if (O->shadow_skip || O->cull == RT_CULL_ALWAYS) continue;
-    if (O->cull == RT_CULL_BOX) CNT(cb + 1);
-    if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, cr, tmax)) continue;
     if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, p, dir, tmax)) continue;
     CNT(cb + 2);
     const double tobj = O->transparency;
