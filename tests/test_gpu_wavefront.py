@@ -139,3 +139,19 @@ def test_ray_tree_autotune_same_pixels(worldmap, name, t):
     _, ru = O.OracleScene(scene_text(name), t, W, H).render(0, H)
     for k, f in enumerate(frames):
         assert_close(f, None, ru, None, f"{name} t={t} auto launch {k}")
+
+
+@pytest.mark.parametrize("pairs", [1, 2])
+@pytest.mark.parametrize("text,d", [
+    ("draw(sphere(<0, 0, 0>, 30, red, 0.3, 0.6))", 10),                         # one object: a ray tree
+    ("draw(sphere(<0, 0, 0>, 30, red, 0.3, 0.6))\ndraw(plane(<0, 1, 0>, 35, blue, 0.5))", 1),   # depth 1
+    ("draw(plane(<0, 1, 0>, 35, blue, 0.5))", 10),                                # unbounded object only
+])
+def test_wavefront_pairs_small_scenes(text, d, pairs):
+    """Pair-path edge cases: a single object (one bucket), depth 1 (one pair level), an unbounded
+    object (no culling box) -- every frame against the oracle."""
+    from oracle import oracle as O
+    W, H = 96, 72
+    gu, gf = _render(text, 0.0, W, H, d, pairs=pairs)
+    rf, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H, f64=True)
+    assert_close(gu, gf, ru, rf, f"wavefront pairs={pairs} small scene d={d}")
