@@ -126,3 +126,7 @@ def test_shadow_pow_flag():
     assert pw(open(os.path.join(SCENES, "spinning_globes.scene")).read(), 0.3) == 1
     assert pw("draw(sphere(<0, 0, 0>, 30, red, 0, 0.5))\ndraw(sphere(<0, 9, 0>, 3, red, 0, 1))") == 1
     assert pw("draw(sphere(<0, 0, 0>, 30, red, 0, 0.5))\ndraw(sphere(<0, 9, 0>, 3, red, 0, 0.25))") == 0
+    # -0 is a zero factor (the product is 0 at it, whatever the order); 1 is skipped
+    assert pw("draw(sphere(<0, 0, 0>, 30, red, 0, 0.5))\ndraw(sphere(<0, 9, 0>, 3, red, 0, 0 * (0 - 1)))") == 1
+    assert pw("draw(sphere(<0, 0, 0>, 30, red, 0, 0.5))\ndraw(sphere(<0, 9, 0>, 3, red, 0, 0.5))\n"
+              "draw(sphere(<9, 0, 0>, 3, red, 0, 1))") == 1
