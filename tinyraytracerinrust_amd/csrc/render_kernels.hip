@@ -2784,7 +2784,10 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
   const uint32_t nobj = (uint32_t)c->dev.n_objects;
   uint32_t* bins[3] = {P.bins, P.bins + 4096, P.bins + 8192};
   for (;;) {
-    const dim3 ge(std::min<uint32_t>((P.cap + 63) / 64, (uint32_t)c->n_cu * 32u));   // grid-stride evaluations
+    // grid-stride evaluations: one pass covers ~4 pairs per ray of the level (fractal: ~3), capped at
+    // 8 waves per SIMD -- small levels then launch hundreds, not thousands, of idle workgroups
+    const dim3 ge(std::max<uint32_t>((uint32_t)c->n_cu, std::min<uint32_t>((uint32_t)(((size_t)n * 4 + 63) / 64),
+                                                                          (uint32_t)c->n_cu * 32u)));
     RT_HIP(hipMemsetAsync(P.count, 0, 8, st));
     RT_HIP(hipMemsetAsync(P.bins, 0, 3 * 16384, st));        // the three sorts' bucket counters
     hipLaunchKernelGGL((wfp_cand_kernel<false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
