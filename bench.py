@@ -224,17 +224,57 @@ def issue_model(config, world, layout, kernel_ms, n_cu=256, clock_ghz=2.4):
     return out
 
 
-def executed_fp64(config, world, layout, kernel_ms):
+def lib_sha16():
+    """sha256 (16 hex digits) of the loaded librt_mi355x.so: the binary a PMC block must come from."""
+    import hashlib
+    from tinyraytracerinrust_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def executed_fp64(config, world, layout, kernel_ms, variant=None):
     """The EXECUTED FP64 rate: (ADD + MUL + 2 FMA) wave-instructions x 64 per launch from the PMC
-    summary over this run's kernel time -- the hardware's view, next to `roofline.achieved` (the
-    reference algorithm's flops, of which exact culling skips about 60 %)."""
+    summary over this run's kernel time -- the hardware's view (`roofline.frac`), next to the reference
+    algorithm's flops (`frac_algorithmic`, of which exact culling skips about 70 %).  The block names
+    the session and the library binary the counters were measured on, and whether that binary (and
+    kernel variant) is the one this run loaded."""
     e = load_pmc(config, world, layout)
     fl = e.get("executed_fp64_flops_per_launch")
     if not fl or not kernel_ms:
         return None
     tf = fl / (kernel_ms * 1e-3) / 1e12
+    sha = lib_sha16()
+    same = e.get("so_sha16") == sha and (variant is None or e.get("variant", "generic") == variant)
     return {"tflops": round(tf, 3), "frac": round(tf / FP64_VECTOR_PEAK_TFLOPS, 4),
-            "flops_per_launch": fl, "pmc_tag": e.get("tag"), "valu_insts_per_wave": e.get("valu_insts_per_wave")}
+            "flops_per_launch": fl, "pmc_tag": e.get("tag"), "pmc_so_sha16": e.get("so_sha16"),
+            "pmc_variant": e.get("variant", "generic"), "this_so_sha16": sha, "pmc_matches_binary": same,
+            "valu_insts_per_wave": e.get("valu_insts_per_wave")}
+
+
+def roofline_block(achieved_alg, ex, traffic, extra):
+    """`roofline` of a bench line.  `frac` is a HARDWARE fraction: the FP64 flops the render kernel
+    executes (PMC: (ADD + MUL + 2 FMA) x 64 per launch, `executed_fp64`) per second of this run's
+    kernel time over the 78.6 TFLOP/s FP64 peak.  The reference algorithm's flop count (the oracle's
+    counting build) over the same time is `achieved_algorithmic` / `frac_algorithmic`: it exceeds what
+    the GPU executes, because exact culling skips most of the reference's work, so it says how fast
+    the reference's computation is delivered, not how busy the hardware is (round-3 VERDICT)."""
+    hw = ex["tflops"] if ex else None
+    out = {
+        "bound": "fp64-valu",
+        "achieved": hw,
+        "peak": FP64_VECTOR_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(hw / FP64_VECTOR_PEAK_TFLOPS, 4) if hw else None,
+        "frac_basis": "executed FP64 flops (PMC, executed_fp64) / this run's kernel time / FP64 peak",
+        "traffic": traffic,
+        "achieved_algorithmic": round(achieved_alg, 3) if achieved_alg else None,
+        "frac_algorithmic": round(achieved_alg / FP64_VECTOR_PEAK_TFLOPS, 4) if achieved_alg else None,
+        "frac_of_no_fma_ceiling": round(achieved_alg / FP64_NO_FMA_TFLOPS, 4) if achieved_alg else None,
+        "no_fma_ceiling": FP64_NO_FMA_TFLOPS,
+        "executed_fp64": ex,
+    }
+    out.update(extra)
+    return out
 
 
 def cpu_baseline(text, W, H, t, depth, threads, target_s=1.0):
@@ -488,6 +528,8 @@ def main():
         T.write_png(a.png, frames[(a.warmup + a.steps - 1) % nbuf].cpu().numpy())
 
     if rank != 0:
+        for h in hw + ([ahw] if ahw else []):
+            h.close()
         if multi:
             dist.destroy_process_group()
         return
@@ -497,6 +539,7 @@ def main():
     flops_launch = sum(fl["row_flops"][y] for y in rows_rendered) if fl else None
     achieved = flops_launch / (busy_ms * 1e-3) / 1e12 if flops_launch else None
     traffic = load_traffic(a.config, world, layout)
+    ex = executed_fp64(a.config, world, layout, busy_ms, rend.kernel_variant())
     # algorithmic bytes of one launch: its RGBA8 rows written + scene blob + the texture once
     alg_bytes = len(rows_rendered) * W * 4 + 1024 * 568 * 4 + 16 * 1024
     line = {
@@ -528,25 +571,16 @@ def main():
             "frame_bytes": W * H * 4,
         },
         "rays": rays_line(fl, W * H * a.steps / elapsed),
-        "roofline": {
-            "bound": "fp64-valu",
-            "achieved": round(achieved, 3) if achieved else None,
-            "peak": FP64_VECTOR_PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4) if achieved else None,
-            "traffic": traffic,
-            "kernel": "render_rows_kernel",
+        "roofline": roofline_block(achieved, ex, traffic, {
+            "kernel": rend.kernel_info(),
             "kernel_ms_mean": round(mean_kernel_ms, 4),
             "achieved_basis": ("kernel time: one event pair over the K back-to-back launches on the launch stream / K"
                                if region else "kernel event time per launch" if K == 1
                                else f"step wall time ({K} frames in flight; no per-step events)"),
             "kernel_ms_min": round(min(kernel_ms), 4) if per_step else None,
             "algorithmic_flops_per_launch": flops_launch,
-            "frac_of_no_fma_ceiling": round(achieved / FP64_NO_FMA_TFLOPS, 4) if achieved else None,
-            "no_fma_ceiling": FP64_NO_FMA_TFLOPS,
-            "executed_fp64": executed_fp64(a.config, world, layout, busy_ms),
             "issue": issue_model(a.config, world, layout, busy_ms),
-        },
+        }),
         "roofline_hbm": {
             "bound": "hbm",
             "achieved": round(alg_bytes / (busy_ms * 1e-3) / 1e9, 2),
@@ -583,11 +617,10 @@ def main():
         line["cpu_baseline"] = cb
     json_out.write(json.dumps(line) + "\n")
     json_out.flush()
+    for h in hw + ([ahw] if ahw else []):
+        h.close()
     if multi:
         dist.destroy_process_group()
-
-
-_KEEP = []
 
 
 def inflight_phase(T, rend, stream, dev, frame, whole, H, W, depth, local, K, steps):
@@ -612,7 +645,8 @@ def inflight_phase(T, rend, stream, dev, frame, whole, H, W, depth, local, K, st
     if bad:
         raise SystemExit(f"inflight phase: frame buffer(s) {bad} differ from the single-launch render")
     rend.set_kernel("auto")
-    _KEEP.extend(hw)             # the streams live until the process exits (as the main pipeline's)
+    for h in hw:                 # synchronise and destroy them now, not at the runtime's teardown
+        h.close()
     return {"frames_in_flight": K, "steps": steps, "ms_per_step": round(el * 1e3 / steps, 4),
             "value": round(W * H * steps / el / 1e6, 2), "kernel": "megakernel (rt_ctx_set_option)",
             "frame_check": f"all {K} frame buffers == single-launch render",
@@ -835,6 +869,8 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
         counts = [None] * world
         dist.all_gather_object(counts, mine)
         frames_per_rank = counts
+    for h in hw:
+        h.close()
     if rank != 0:
         if multi:
             dist.destroy_process_group()
@@ -842,6 +878,7 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
     path = os.path.join(ROOT, "tests", "golden", f"flops_{scene}_{W}x{H}_anim{F}_d{depth}.json")
     fl = json.load(open(path)) if os.path.exists(path) else None
     achieved = None
+    busy_frame_ms = (sum(per_frame) / len(per_frame)) if K == 1 else elapsed * 1e3 / a.steps / len(mine)
     if fl:
         # One stream: the frames' kernel time (events on the launch stream).  Several streams:
         # the kernels overlap, so the flops are divided by the step's wall time instead.
@@ -869,25 +906,17 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
             "kernel": a.kernel,
             "collective": None,
         },
-        "roofline": {
-            "bound": "fp64-valu",
-            "achieved": round(achieved, 3) if achieved else None,
-            "peak": FP64_VECTOR_PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 4) if achieved else None,
-            "traffic": load_traffic(a.config, 1, "contiguous"),     # HBM bytes per frame (PMC, profiles/)
-            "kernel": "render_rows_kernel<RT_MODE_CHAIN> (ray-chain scene; RT_OPT_KERNEL " + a.kernel + ")",
+        "roofline": roofline_block(achieved, executed_fp64(a.config, 1, "contiguous", busy_frame_ms,
+                                                            rends[0].kernel_variant()),
+                                   load_traffic(a.config, 1, "contiguous"), {
+            "kernel": rends[0].kernel_info() + " (ray-chain scene; RT_OPT_KERNEL " + a.kernel + ")",
             "streams": K,
             "achieved_basis": "kernel event time" if K == 1 else "step wall time (frames overlap on the streams)",
             "kernel_ms_mean": round(sum(per_frame) / len(per_frame), 4),
             "kernel_ms_min": round(min(per_frame), 4),
             "kernel_ms_max": round(max(per_frame), 4),
-            "executed_fp64": executed_fp64(a.config, 1, "contiguous",
-                                           (sum(per_frame) / len(per_frame)) if K == 1 else elapsed * 1e3 / a.steps / len(mine)),
-            "frac_of_no_fma_ceiling": round(achieved / FP64_NO_FMA_TFLOPS, 4) if achieved else None,
-            "issue": issue_model(a.config, 1, "contiguous",
-                                 (sum(per_frame) / len(per_frame)) if K == 1 else elapsed * 1e3 / a.steps / len(mine)),
-        },
+            "issue": issue_model(a.config, 1, "contiguous", busy_frame_ms),
+        }),
         "rays": rays_line(fl, F * W * H * a.steps / elapsed),
         "host_compile_upload_ms_per_frame": round(prep_ms, 3),
         "settle": settle,

@@ -132,6 +132,10 @@ int rt_scene_get_camera(const rt_scene* scene, double out[13]);
  * pre-order, node i = (obj[i], skip[i]); obj = -1 for a group node, skip = index after the
  * node's subtree.  Object nodes appear in draw order.  Writes min(n, cap) nodes; *n = total. */
 int rt_scene_traversal(const rt_scene* scene, int32_t* obj, int32_t* skip, int32_t cap, int32_t* n);
+/* The flattened scene as text (tests, debugging; no reference counterpart): the kernel-choice
+ * flags, both object hierarchies and every object's and leaf's culling record -- what
+ * rt_ctx_upload would put in HBM.  Writes at most cap - 1 bytes and a NUL; *len = full length. */
+int rt_scene_describe(const rt_scene* scene, char* buf, size_t cap, size_t* len);
 /* Light i: point[3] (world space, as stored by add_light) and color[4]. */
 int rt_scene_get_light(const rt_scene* scene, int32_t i, double point[3], double color[4]);
 void rt_scene_free(rt_scene* scene);
@@ -262,15 +266,35 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  * hierarchy for 64 rays (wf_trace_kernel); 1 (default) levels >= 1 go through (ray, object) pairs
  * sorted by object, so a wave tests one object against 64 rays (wfp_* kernels; scenes whose shadow
  * products are order-free, RtDevScene::shadow_pow, and fewer than 4096 objects; else as 0); 2 level 0
- * (the camera rays) too. */
+ * (the camera rays) too.  The wavefront path synchronises the host with the launch stream once per
+ * recursion level (it reads each level's ray count), and RT_KERNEL_AUTO's first ordered launch of a
+ * ray-tree geometry times one wavefront launch against the megakernel (blocking, once): such
+ * launches return only after the work is done, even with device output.
+ * RT_OPT_SPECIALIZE: 0 (default) the library's precompiled kernels; 1 also compiles the uploaded
+ * scene's row kernels with the scene's tables as constants (hipRTC, spec.hip: the hierarchy walk
+ * unrolled, every record field a literal; same pixels) for RGBA8 / RGB8 launches; 2 for the f64
+ * and calibration launches too.  The compile runs on the calling thread at
+ * rt_ctx_upload (or here, when a scene is already uploaded): seconds of host time per new scene (the
+ * code object is cached per process by the program text), so it pays for hosts that render many
+ * frames of one scene.  Launches whose kernel has no specialised form (wavefront, refraction
+ * deferred, RT_OPT_FAST_CLAMP 0 on a min/max-clamp scene) keep the generic kernels. */
 typedef enum rt_option {
   RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4,
-  RT_OPT_WAVEFRONT_PAIRS = 5
+  RT_OPT_WAVEFRONT_PAIRS = 5, RT_OPT_SPECIALIZE = 6
 } rt_option;
 typedef enum rt_kernel_choice {
   RT_KERNEL_AUTO = 0, RT_KERNEL_MEGA = 1, RT_KERNEL_DEFERRED = 2, RT_KERNEL_WAVEFRONT = 3
 } rt_kernel_choice;
 int rt_ctx_set_option(rt_ctx* ctx, int32_t option, int32_t value);
+/* What the context's row launches run, as text: "generic (librt_mi355x.so)" or the specialised
+ * program's hash, mode and compile time, and which kernel the last row launch took. */
+int rt_ctx_kernel_info(rt_ctx* ctx, char* buf, size_t cap);
+/* Compile the scene's specialised program (RT_OPT_SPECIALIZE) into the process's code-object
+ * cache without a device, so a later upload of the same scene finds it; *compile_ms = the hipRTC
+ * time (0 when it was cached already).  May run on any thread. */
+int rt_scene_precompile(const rt_scene* scene, double* compile_ms);
+/* The specialised program's text (tests, debugging): cap, len as rt_scene_describe. */
+int rt_scene_spec_program(const rt_scene* scene, char* buf, size_t cap, size_t* len);
 void rt_ctx_free(rt_ctx* ctx);
 /* A HIP stream on a hardware queue of its own (hipExtStreamCreateWithCUMask with every CU
  * enabled), for renders that overlap: plain streams share the process's few hardware queues

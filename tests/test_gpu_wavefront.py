@@ -63,6 +63,30 @@ def test_wavefront_pairs_one_object_many_hits(worldmap):
         assert_close(gu, gf, ru, rf, f"wavefront shells pairs={pairs}")
 
 
+HUGE_T_SCENE = (
+    "b = (1000000000 * 1000000000)\n"
+    "t = ((b * b) * (b * b))\n"                           # 1e72: T^k overflows to inf after 5 hits
+    "draw(sphere(<0, 0, -40>, 30, rgb(0.9, 0.9, 0.9), 0, t))\n"
+    "draw(sphere(<0, 0, -40>, 25, rgb(0.9, 0.5, 0.5), 0, t))\n"
+    "draw(sphere(<0, 0, -40>, 20, rgb(0.5, 0.9, 0.5), 0, t))\n"
+    "draw(sphere(<0, 0, 10>, 12, rgb(0.5, 0.5, 0.9), 0.5))\n"
+    "draw(plane(<0, 1, 0>, 40, blue, 0.3))\n"
+    "append light(<0, 80, -160>, rgb(0.6, 0.6, 0.6), 100)\n")
+
+
+def test_wavefront_huge_transparency_shadow_order(worldmap):
+    """Shadow rays through shells of transparency 1e72 and an opaque sphere: in draw order the product
+    reaches inf before or after the opaque factor (inf * 0 = NaN, which is not 0: the light still
+    counts), so it is not a function of the hit counts and the pair path must not fold counts
+    (scene.cpp shadow_pow).  Every pair setting against the oracle."""
+    from oracle import oracle as O
+    W, H, d = 160, 120, 6
+    rf, ru = O.OracleScene(HUGE_T_SCENE, 0.0, W, H, max_depth=d).render(0, H, f64=True)
+    for pairs in (0, 1, 2):
+        gu, gf = _render(HUGE_T_SCENE, 0.0, W, H, d, pairs=pairs)
+        assert_close(gu, gf, ru, rf, f"wavefront huge transparency pairs={pairs}")
+
+
 @pytest.mark.parametrize("pairs", [0, 2])
 @pytest.mark.parametrize("name,t", [("fractal", 0.0), ("spinning_globes", 0.3), ("globes", 0.0)])
 def test_wavefront_level_overflow_fixup(worldmap, name, t, pairs):

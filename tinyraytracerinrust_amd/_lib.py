@@ -25,6 +25,7 @@ RT_OPT_TILE_ORDER = 2
 RT_OPT_FAST_CLAMP = 3
 RT_OPT_WAVEFRONT_CAP = 4
 RT_OPT_WAVEFRONT_PAIRS = 5
+RT_OPT_SPECIALIZE = 6
 RT_KERNEL_AUTO, RT_KERNEL_MEGA, RT_KERNEL_DEFERRED, RT_KERNEL_WAVEFRONT = 0, 1, 2, 3
 
 
@@ -76,6 +77,10 @@ SIGNATURES = {
                               ctypes.POINTER(_P)]),
     "rt_scene_traversal": (_I, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
                                 ctypes.POINTER(ctypes.c_int32)]),
+    "rt_scene_describe": (_I, [_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+    "rt_scene_spec_program": (_I, [_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+    "rt_scene_precompile": (_I, [_P, ctypes.POINTER(ctypes.c_double)]),
+    "rt_ctx_kernel_info": (_I, [_P, ctypes.c_char_p, ctypes.c_size_t]),
     "rt_scene_info": (_I, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_U32),
                            ctypes.POINTER(_U32)]),

@@ -1,0 +1,916 @@
+// k_wavefront.hip -- the wavefront path (one recursion depth per pass over a dense level of rays)
+// and its pair path ((ray, object) work items sorted by object), launch-wide secondary-ray
+// compaction for ray-tree scenes (DESIGN.md §2 "Wavefront path").  get_ray_color's operations per
+// ray are rt_device.h's; this file reorganises WHEN they run, never what they compute.
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+
+#include "rt_device.h"
+#include "rt_ctx.h"
+
+namespace {
+
+// ====================================================================== wavefront path
+// get_ray_color (raytracer.rs:132-287) launch-wide, one bounce level per pass: level d holds every
+// ray of recursion depth d of the launch, densely, one lane per ray.  Per level:
+//   wf_trace_kernel  nearest hit, shadow rays, shading, the inside / refraction / TIR / reflection
+//                    decisions of trace() (the same operations in the same order); the rays a hit
+//                    spawns are appended to level d + 1 (one ballot + one atomic per wave), each with a
+//                    coherence key (direction octant, Morton code of its origin); the hit record (L,
+//                    the two weights, the children's slots) stays at the ray's slot;
+//   sort             level d + 1's slots by key (rocPRIM radix sort of (key, slot) pairs): a wave of
+//                    the next pass then traces rays that start close together in similar directions,
+//                    so the wave-coherent traversal walks fewer objects (the megakernel's waves walk the
+//                    union of what their lanes' scattered secondary rays need);
+//   wf_fold_kernel   after every level is traced, from the deepest level up: a ray's colour from its
+//                    hit record and its children's colours (already folded into their L slots):
+//                      refraction child: comb = in_range(L.intensify(1 - t) + C_t.intensify(t)),
+//                      then a reflection child: in_range(comb.intensify(1 - rp) + C_r.intensify(rp)),
+//                    exactly the post-order of raytracer.rs:256-279 (trace()'s frame fold).  Level 0's
+//                    fold writes the pixels.
+// Lanes whose pixel's tree ended early no longer idle in its wave (the megakernel's per-lane tree
+// walk keeps a wave alive for its deepest tree): every pass starts with every lane on a live ray, and
+// every pass is one workgroup per 64 rays, so the hardware dispatcher balances uneven rays.  The
+// host reads each level's count before launching it (one synchronisation per level: this path is
+// for heavy, incoherent launches).  Levels >= 1 hold RT_OPT_WAVEFRONT_CAP % of the pixel slots; a
+// ray that finds its level full marks its pixel, and wf_fixup_kernel re-renders marked pixels with
+// trace() (same bits).
+struct WfArena {
+  uint8_t* base;          // level tables (wf_level)
+  uint32_t* count;        // count[d]: rays appended to level d (d >= 1); count[RT_MAX_DEPTH_CAP + 2]: any overflow
+  uint8_t* ovf;           // per pixel slot: its tree overflowed a level
+  const uint32_t* perm;   // the level being traced: slot of its i-th ray in key order (null: slot order)
+  uint32_t slots, cap;    // level 0 = the pixel slots (8x8 tiles x 64), levels >= 1: cap rays each
+  double klo[3], kscale[3];   // origin -> 9-bit cell per axis for the coherence keys
+};
+struct WfLevel {
+  double *ox, *oy, *oz, *dx, *dy, *dz;   // levels >= 1: the ray
+  double *Lr, *Lg, *Lb, *wt, *wr;        // hit record: L (then the folded colour), refraction / reflection weights
+  int32_t *pix, *ct, *cr;                // pixel slot (levels >= 1), children's slots in level d + 1 (-1: none)
+  uint32_t *key, *val;                   // levels >= 1: coherence key and slot (the sort's input pairs)
+  int32_t* par;                          // levels >= 1: the object whose hit spawned the ray
+};
+constexpr size_t RT_WF_BYTES0 = 5 * 8 + 2 * 4, RT_WF_BYTES = 11 * 8 + 6 * 4;
+__host__ __device__ __forceinline__ WfLevel wf_level(const WfArena& A, int d) {
+  WfLevel v;
+  const size_t len = d == 0 ? A.slots : A.cap;
+  double* f = (double*)(A.base + (d == 0 ? 0 : (size_t)A.slots * RT_WF_BYTES0 + (size_t)(d - 1) * A.cap * RT_WF_BYTES));
+  if (d == 0) {
+    v.ox = v.oy = v.oz = v.dx = v.dy = v.dz = nullptr;
+    v.Lr = f; v.Lg = f + len; v.Lb = f + 2 * len; v.wt = f + 3 * len; v.wr = f + 4 * len;
+    int32_t* q = (int32_t*)(f + 5 * len);
+    v.pix = nullptr; v.ct = q; v.cr = q + len;
+    v.key = v.val = nullptr;
+    v.par = nullptr;
+  } else {
+    v.ox = f; v.oy = f + len; v.oz = f + 2 * len; v.dx = f + 3 * len; v.dy = f + 4 * len; v.dz = f + 5 * len;
+    v.Lr = f + 6 * len; v.Lg = f + 7 * len; v.Lb = f + 8 * len; v.wt = f + 9 * len; v.wr = f + 10 * len;
+    int32_t* q = (int32_t*)(f + 11 * len);
+    v.pix = q; v.ct = q + len; v.cr = q + 2 * len;
+    v.key = (uint32_t*)(q + 3 * len); v.val = (uint32_t*)(q + 4 * len);
+    v.par = q + 5 * len;
+  }
+  return v;
+}
+// pixel slot -> (x, output row r); false outside the launch's rows / frame
+__device__ __forceinline__ bool wf_pixel(const RtDevScene& S, uint32_t slot, int y_first, int band_rows, int band_pitch,
+                                         int n_rows, int* x, int* r, int* y) {
+  const unsigned tiles_x = (unsigned)(S.width + 7) / 8, tile = slot >> 6, l = slot & 63;
+  *x = (int)(tile % tiles_x) * 8 + (int)(l & 7);
+  *r = (int)(tile / tiles_x) * 8 + (int)(l >> 3);
+  if (*x >= S.width || *r >= n_rows) return false;
+  *y = y_first + (*r / band_rows) * band_pitch + *r % band_rows;
+  return *y < S.height;
+}
+// coherence key of a ray: direction octant (3 bits) above the 27-bit Morton code of its origin's
+// cell (9 bits per axis over the scene's bounded extent, clamped).  Only the processing order
+// depends on it, never a value.
+__device__ __forceinline__ uint32_t wf_spread9(uint32_t v) {            // 9 bits -> every third bit
+  v &= 511u;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+__device__ __forceinline__ uint32_t wf_key(const WfArena& A, V3 o, V3 d) {
+  auto cell = [](double x, double lo, double sc) -> uint32_t {
+    const double c = (x - lo) * sc;
+    return c > 0.0 ? (c < 511.0 ? (uint32_t)c : 511u) : 0u;           // NaN -> 0
+  };
+  const uint32_t oct = (d.x < 0.0 ? 1u : 0u) | (d.y < 0.0 ? 2u : 0u) | (d.z < 0.0 ? 4u : 0u);
+  return (oct << 27) | wf_spread9(cell(o.x, A.klo[0], A.kscale[0])) | (wf_spread9(cell(o.y, A.klo[1], A.kscale[1])) << 1) |
+         (wf_spread9(cell(o.z, A.klo[2], A.kscale[2])) << 2);
+}
+
+// One ray of trace()'s loop body: nearest hit, the light loop (shadow rays first, then the shading
+// inputs), the inside test and the refraction / reflection decisions (raytracer.rs:141-280).
+// NH(&t) gives the nearest hit (object, distance), SH(k, p, sdir, dist) light k's shadow
+// transparency: the traversals themselves (wf_ray) or the pair path's folded results (wfp_shade).
+template <bool REFR, bool FC, class NH, class SH>
+__device__ __forceinline__ void wf_ray_core(const DS& S, V3 ro, V3 rd, int depth, int max_depth, NH&& nh, SH&& sh,
+                                            Col* Lo, double* wt, double* wr, bool* ch_t, bool* ch_r, V3* po, V3* dt,
+                                            V3* dr) {
+  *ch_t = *ch_r = false;
+  *Lo = {0.0, 0.0, 0.0};
+  *wt = *wr = 0.0;
+  double t_hit;
+  const int oi = nh(&t_hit);
+  if (oi < 0) return;                                                   // Color::BLACK (:152-160)
+  const V3 p = add(ro, scale(rd, t_hit));                               // :162
+  V3 nrm = {0.0, 0.0, 0.0};
+  Col c = {0.0, 0.0, 0.0}, L = {0.0, 0.0, 0.0};
+  double transp = 0.0, refl = 0.0;
+  bool have_shading = false;
+#pragma unroll 1
+  for (int k = 0; k < S.n_lights; ++k) {                                // :175-228, as trace()
+    cptr<RtLight> lt = &S.lights[k];
+    const V3 lv = sub(ld3(lt->p), p);
+    double ll, ill;
+    len_inv(lv, &ll, &ill);
+    const V3 sdir = scale(lv, ill);
+    const double t = sh(k, p, sdir, ll);
+    if (!have_shading) {
+      shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
+      L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));
+      have_shading = true;
+    }
+    if (t == 0.0) continue;
+    double ang = rt_acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
+    if (ang >= PI_D / 2.0) ang = PI_D - ang;
+    const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
+    const Col lc = intensify<FC>(intensify<FC>(Col{lt->col[0], lt->col[1], lt->col[2]}, inten), t);
+    L = cadd<FC>(L, cmul<FC>(c, lc));
+  }
+  if (!have_shading) {
+    shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
+    L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));
+  }
+  bool inside = false;                                                  // :230-235
+  if (depth < max_depth && (refl != 0.0 || (REFR && transp != 0.0))) {
+    const V3 nd = scale(rd, -1.0);
+    inside = inside_test(dot(nd, nrm) / (len(nd) * len(nrm)));
+  }
+  const V3 n2 = inside ? scale(nrm, -1.0) : nrm;
+  const double r1 = inside ? 1.45 : 1.0, r2 = inside ? 1.0 : 1.45;
+  bool tir = false;
+  V3 tdir = {0.0, 0.0, 0.0};
+  const bool do_refr = REFR && depth < max_depth && transp != 0.0;     // :242
+  if (do_refr) tdir = refract_dir(rd, n2, r1 / r2, &tir);
+  const double rp = tir ? refl + (1.0 - refl) * transp : refl;         // :261-265
+  const bool do_refl = depth < max_depth && rp != 0.0 && (!inside || tir);   // :267
+  *Lo = L;
+  *wt = transp;
+  *wr = rp;
+  *ch_t = do_refr && !tir;
+  *ch_r = do_refl;
+  *po = p;
+  *dt = tdir;
+  if (do_refl) *dr = reflect_dir(rd, n2);
+}
+
+template <bool REFR, bool FC>
+__device__ __forceinline__ void wf_ray(const DS& S, V3 ro, V3 rd, int depth, int max_depth, Col* Lo, double* wt,
+                                       double* wr, bool* ch_t, bool* ch_r, V3* po, V3* dt, V3* dr, int* hit_obj) {
+  constexpr bool SHARE = REFR && RT_SPHERE_SHARE, OBB = !REFR;
+  wf_ray_core<REFR, FC>(
+      S, ro, rd, depth, max_depth,
+      [&](double* t) { return *hit_obj = nearest_hit<SHARE, OBB>(S, ro, rd, t); },
+      [&](int, V3 p, V3 sdir, double ll) { return shadow_transparency<SHARE, OBB>(S, p, sdir, ll); }, Lo, wt, wr, ch_t,
+      ch_r, po, dt, dr);
+}
+
+// The rays a wave's hits spawn, appended to level d + 1 (one ballot per kind, ONE atomic per
+// wave: the wave's refraction children, then its reflection children, in lane order), and the hit
+// record at the ray's slot j.
+__device__ __forceinline__ void wf_append(const WfArena& A, const WfLevel& lv, int d, int lane, bool live, uint32_t j,
+                                          int32_t pix, Col L, double wt, double wr, bool ch_t, bool ch_r, V3 p, V3 dt,
+                                          V3 dr, int32_t par = -1) {
+  int32_t ct = -1, cr = -1;
+  const uint64_t bt = __ballot(ch_t), br = __ballot(ch_r);
+  const uint32_t nt = (uint32_t)__popcll(bt), nr = (uint32_t)__popcll(br);
+  if (nt + nr) {                                             // wave-uniform: d < max_depth here
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t b0 = 0;
+    if (lane == 0) b0 = atomicAdd(&A.count[d + 1], nt + nr);
+    b0 = (uint32_t)__shfl((int)b0, 0);
+    const WfLevel nx = wf_level(A, d + 1);
+    const uint32_t st = b0 + (uint32_t)__popcll(bt & below), sr = b0 + nt + (uint32_t)__popcll(br & below);
+    bool ovf = false;
+    if (ch_t) {
+      if (st < A.cap) {
+        nx.ox[st] = p.x; nx.oy[st] = p.y; nx.oz[st] = p.z; nx.dx[st] = dt.x; nx.dy[st] = dt.y; nx.dz[st] = dt.z;
+        nx.pix[st] = pix; nx.key[st] = wf_key(A, p, dt); nx.val[st] = st; nx.par[st] = par;
+        ct = (int32_t)st;
+      } else ovf = true;
+    }
+    if (ch_r) {
+      if (sr < A.cap) {
+        nx.ox[sr] = p.x; nx.oy[sr] = p.y; nx.oz[sr] = p.z; nx.dx[sr] = dr.x; nx.dy[sr] = dr.y; nx.dz[sr] = dr.z;
+        nx.pix[sr] = pix; nx.key[sr] = wf_key(A, p, dr); nx.val[sr] = sr; nx.par[sr] = par;
+        cr = (int32_t)sr;
+      } else ovf = true;
+    }
+    if (ovf) {                                                // this pixel is re-rendered by wf_fixup_kernel
+      A.ovf[pix] = 1;
+      A.count[RT_MAX_DEPTH_CAP + 2] = 1;
+    }
+  }
+  if (live) {
+    lv.Lr[j] = L.r; lv.Lg[j] = L.g; lv.Lb[j] = L.b; lv.wt[j] = wt; lv.wr[j] = wr;
+    lv.ct[j] = ct; lv.cr[j] = cr;
+  }
+}
+
+#ifndef RT_WAVES_PER_EU_WF
+#define RT_WAVES_PER_EU_WF 5
+#endif
+// One workgroup (wave) per 64 rays of level d (n of them): level 0 = the pixel slots in tile order,
+// levels >= 1 in key order (A.perm).
+template <bool REFR, bool FC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_WF))) void wf_trace_kernel(
+    RtDevScene S, WfArena A, int d, uint32_t n, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+  bool live = i < n;
+  const WfLevel lv = wf_level(A, d);
+  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+  uint32_t j = i;                                            // the ray's slot in its level
+  int32_t pix = (int32_t)i;
+  if (d == 0) {
+    int x, r, y;
+    live = live && wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y);
+    if (live) camera_ray(S.cam, (double)x, (double)y, &ro, &rd);          // get_pixel(x as f64, y as f64)
+  } else if (live) {
+    j = A.perm ? A.perm[i] : i;
+    ro = {lv.ox[j], lv.oy[j], lv.oz[j]};
+    rd = {lv.dx[j], lv.dy[j], lv.dz[j]};
+    pix = lv.pix[j];
+  }
+  Col L = {0.0, 0.0, 0.0};
+  double wt = 0.0, wr = 0.0;
+  bool ch_t = false, ch_r = false;
+  V3 p = {0.0, 0.0, 0.0}, dt = {0.0, 0.0, 0.0}, dr = {0.0, 0.0, 0.0};
+  int oi = -1;
+  if (live) wf_ray<REFR, FC>(make_ds(S), ro, rd, d, max_depth, &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr, &oi);
+  wf_append(A, lv, d, lane, live, j, pix, L, wt, wr, ch_t, ch_r, p, dt, dr, oi);
+}
+
+template <bool F64, bool FC>
+__global__ __launch_bounds__(256) void wf_fold_kernel(RtDevScene S, WfArena A, int d, uint32_t n, int y_first,
+                                                      int band_rows, int band_pitch, int n_rows,
+                                                      uint8_t* __restrict__ out, size_t stride, int rgb) {
+  const WfLevel lv = wf_level(A, d);
+  const WfLevel ch = wf_level(A, d + 1);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int x = 0, r = 0, y = 0;
+    if (d == 0 && (!wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y) || A.ovf[i])) continue;
+    const Col L = {lv.Lr[i], lv.Lg[i], lv.Lb[i]};
+    const int32_t ct = lv.ct[i], cr = lv.cr[i];
+    Col C = L;
+    if (ct >= 0) {                                             // refraction, then a pending reflection
+      const double t = lv.wt[i];
+      C = cadd<FC>(intensify<FC>(L, 1.0 - t), intensify<FC>(Col{ch.Lr[ct], ch.Lg[ct], ch.Lb[ct]}, t));
+    }
+    if (cr >= 0) {
+      const double w = lv.wr[i];
+      C = cadd<FC>(intensify<FC>(C, 1.0 - w), intensify<FC>(Col{ch.Lr[cr], ch.Lg[cr], ch.Lb[cr]}, w));
+    }
+    if (d > 0) {
+      lv.Lr[i] = C.r; lv.Lg[i] = C.g; lv.Lb[i] = C.b;
+      continue;
+    }
+    uint8_t* row = out + (size_t)r * stride;
+    if constexpr (F64) {
+      double* o = (double*)row + (size_t)x * 4;
+      o[0] = C.r; o[1] = C.g; o[2] = C.b; o[3] = 1.0;
+    } else if (rgb) {
+      uint8_t* o = row + (size_t)x * 3;
+      o[0] = (uint8_t)to_u8(C.r); o[1] = (uint8_t)to_u8(C.g); o[2] = (uint8_t)to_u8(C.b);
+    } else {
+      ((uint32_t*)row)[x] = to_u8(C.r) | (to_u8(C.g) << 8) | (to_u8(C.b) << 16) | (255u << 24);
+    }
+  }
+}
+
+// Pixels whose tree overflowed a level: the per-lane megakernel trace (same bits).  Returns at once
+// when no level overflowed (one uniform load).
+template <bool REFR, bool F64, bool FC>
+__global__ __launch_bounds__(64) void wf_fixup_kernel(RtDevScene S, WfArena A, int y_first, int band_rows,
+                                                      int band_pitch, int n_rows, int max_depth,
+                                                      uint8_t* __restrict__ out, size_t stride, int rgb) {
+  if (A.count[RT_MAX_DEPTH_CAP + 2] == 0) return;
+  for (uint32_t i = blockIdx.x * 64 + threadIdx.x; i < A.slots; i += gridDim.x * 64) {
+    int x, r, y;
+    if (!A.ovf[i] || !wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y)) continue;
+    V3 ro, rd;
+    camera_ray(S.cam, (double)x, (double)y, &ro, &rd);
+    const Col C = trace<REFR, NoRec, 0, FC>(make_ds(S), ro, rd, max_depth);
+    uint8_t* row = out + (size_t)r * stride;
+    if constexpr (F64) {
+      double* o = (double*)row + (size_t)x * 4;
+      o[0] = C.r; o[1] = C.g; o[2] = C.b; o[3] = 1.0;
+    } else if (rgb) {
+      uint8_t* o = row + (size_t)x * 3;
+      o[0] = (uint8_t)to_u8(C.r); o[1] = (uint8_t)to_u8(C.g); o[2] = (uint8_t)to_u8(C.b);
+    } else {
+      ((uint32_t*)row)[x] = to_u8(C.r) | (to_u8(C.g) << 8) | (to_u8(C.b) << 16) | (255u << 24);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- wavefront pair path
+// A level's rays are incoherent after a few bounces through scenes of many objects (fractal.scene:
+// 171 objects, glass spheres in hollow CSG cubes).  A wave that walks the hierarchy for 64 scattered
+// rays visits the union of their paths: on fractal.scene only 14 % / 22 % of the lanes are active in
+// a secondary / shadow leaf evaluation, and every level's pass takes as long as a wave's walk over
+// most of the scene (0.6-2 ms even for 25 000 rays).  The pair path splits the traversal into
+// (ray, object) work items and evaluates them object by object:
+//   wfp_cand_kernel<false>   per ray: the hierarchy walk with box tests only (no leaf), emitting a
+//                            pair (object, ray) for every object box the ray meets (through a per-wave
+//                            LDS buffer, one atomic per RT_WFP_BUF pairs);
+//   sort                     the pairs by object (rocPRIM radix sort), so a wave evaluates ONE object
+//                            (scalar loads of its leaves, every lane busy) for 64 different rays;
+//   wfp_near_eval_kernel     per pair: the object's nearest accepted distance (leaf tests, CSG filters:
+//                            nearest_hit's object body); atomicMin of its bits into the ray's best;
+//   wfp_near_tie_kernel      per pair at the ray's best distance: atomicMin of the object index.  The
+//                            nearest hit is the least (distance, object) -- exactly nearest_hit's
+//                            draw-order first-wins rule (raytracer.rs:141-150);
+//   wfp_cand_kernel<true>    per ray with a hit and per light: the shadow ray's candidate objects;
+//   sort, wfp_shadow_eval    per pair: the object's filtered hits with EPS < t < dist; a hit of a
+//                            zero-transparency object marks the shadow ray opaque, other hits add to
+//                            its count.  RtDevScene::shadow_pow (scene.cpp) guarantees the product in
+//                            draw order is then 0 or T^count, order-free (raytracer.rs:181-197);
+//   wfp_shade_kernel         per ray: wf_ray_core's shading, refraction and reflection decisions with
+//                            the folded results, then wf_append, as wf_trace_kernel.
+// Every value is computed by the same operations as the traversals; culling stays conservative
+// (the candidate walk tests boxes against the whole ray, tmax = infinity for the nearest hit).
+struct WfPairs {
+  uint32_t *key, *val;          // pairs as emitted: object, ray id (level slot, or slot * n_lights + light)
+  uint32_t *key_s, *val_s;      // sorted by object
+  double* tp;                   // nearest pass: the sorted pair's object's nearest accepted distance
+  uint32_t* count;              // [0] / [1]: pairs the nearest / shadow pass emitted (may exceed cap: the host
+                                //   grows the arena and runs the level again)
+  uint32_t* bins;               // bucket-sort scratch (RT_BS_MAX_BINS words)
+  uint32_t cap;
+  unsigned long long* tmin;     // per ray of the level: nearest accepted distance (bits; +inf: none)
+  int32_t* omin;                // per ray: the least object index at that distance (INT_MAX: none)
+  double *px, *py, *pz;         // per ray: the hit point
+  uint32_t *kcnt, *opq;         // per shadow ray: hits of transparency-T objects / of a zero-transparency one
+  uint32_t *hkey, *hval, *hkey_s, *hperm;   // per ray: hit-point key, slot; sorted: the shadow / shading order
+};
+#ifndef RT_WFP_BUF
+#define RT_WFP_BUF 512          // pairs buffered in LDS per wave before one atomic allocates their slots
+#endif
+constexpr unsigned long long RT_WFP_NONE = 0x7FF0000000000000ull;   // +inf
+constexpr int RT_WFP_COUNT = 32;      // the pair counts' words in WfArena::count (after the level counts)
+static_assert(RT_MAX_DEPTH_CAP + 3 <= RT_WFP_COUNT, "wavefront counter block");
+
+// The object's nearest accepted distance for one ray: nearest_hit's body for one object, its best
+// starting at +inf (the leaf boxes' tmax only shrinks, as share_prev requires).
+__device__ __forceinline__ double wfp_object_nearest(const DS& S, int o, V3 ro, V3 rd, const CullRay& cr) {
+  cptr<RtObject> O = &S.objects[o];
+  const bool fin = wave_finite(ro, rd);
+  double best = INFINITY;
+  SphereShare shr = {0.0, 0.0, 0.0};
+  const int lb = O->leaf_begin, le = lb + O->leaf_count;
+  for (int l = lb; l < le; ++l) {
+    cptr<RtLeaf> L = &S.leaves[l];
+    if (O->leaf_cull) {
+      if (L->cull == RT_CULL_ALWAYS) continue;
+      if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, cull_tmax(best))) continue;
+    }
+    double t0 = 0.0, t1 = 0.0;
+    const int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1, RT_SPHERE_SHARE ? &shr : nullptr);
+    const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && L->filter_const && !isnan(cr.inv.x));
+    if (n >= 1 && t0 > EPS && t0 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) best = t0;
+    if (n >= 2 && t1 > EPS && t1 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t1))))) best = t1;
+  }
+  return best;
+}
+
+// Filtered hits of the object with EPS < t < dist on one shadow ray (shadow_transparency's body for
+// one object); a zero-transparency object stops at its first.
+__device__ __forceinline__ uint32_t wfp_object_shadow(const DS& S, int o, V3 p, V3 dir, double dist, const CullRay& cr) {
+  cptr<RtObject> O = &S.objects[o];
+  const bool fin = wave_finite(p, dir);
+  const double tmax = cull_tmax(dist);
+  const bool zero = O->transparency == 0.0;
+  uint32_t cnt = 0;
+  SphereShare shr = {0.0, 0.0, 0.0};
+  const int lb = O->leaf_begin, le = lb + O->leaf_count;
+  for (int l = lb; l < le; ++l) {
+    cptr<RtLeaf> L = &S.leaves[l];
+    if (O->leaf_cull) {
+      if (L->cull == RT_CULL_ALWAYS) continue;
+      if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
+    }
+    double t0 = 0.0, t1 = 0.0;
+    const int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1, RT_SPHERE_SHARE ? &shr : nullptr);
+    const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && L->filter_const && !isnan(cr.inv.x));
+    if (n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) {
+      ++cnt;
+      if (zero) return cnt;
+    }
+    if (n >= 2 && t1 > EPS && t1 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t1))))) {
+      ++cnt;
+      if (zero) return cnt;
+    }
+  }
+  return cnt;
+}
+
+// Ray of slot j of level d (level 0: the pixel slot's camera ray).
+__device__ __forceinline__ bool wf_get_ray(const RtDevScene& S, const WfLevel& lv, int d, uint32_t j, int y_first,
+                                           int band_rows, int band_pitch, int n_rows, V3* ro, V3* rd) {
+  if (d == 0) {
+    int x, r, y;
+    if (!wf_pixel(S, j, y_first, band_rows, band_pitch, n_rows, &x, &r, &y)) return false;
+    camera_ray(S.cam, (double)x, (double)y, ro, rd);
+    return true;
+  }
+  *ro = {lv.ox[j], lv.oy[j], lv.oz[j]};
+  *rd = {lv.dx[j], lv.dy[j], lv.dz[j]};
+  return true;
+}
+
+// One wave per 64 rays of level d (in key order).  SHADOW = false: every object whose box the ray
+// meets; true: per light, every object whose box the shadow segment meets (objects of transparency 1
+// skipped, as shadow_transparency does).
+// Each lane walks its own path through the hierarchy (per-lane vector loads of one 64-byte RtTrav
+// record per step, which carries the object's box and flags): a wave-uniform walk visits the union
+// of its 64 rays' paths, measured 4-20 % slower here (profiles/r03m_pairs_fractal_timing.txt).
+template <bool SHADOW>
+__global__ __launch_bounds__(64) void wfp_cand_kernel(RtDevScene S, WfArena A, WfPairs P, int d, uint32_t n,
+                                                      int y_first, int band_rows, int band_pitch, int n_rows) {
+  __shared__ uint32_t sk[RT_WFP_BUF], sv[RT_WFP_BUF];
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+  const WfLevel lv = wf_level(A, d);
+  const DS D = make_ds(S);
+  bool live = i < n;
+  uint32_t j = i;
+  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+  if (live) {
+    j = SHADOW ? P.hperm[i] : (d > 0 && A.perm) ? A.perm[i] : i;
+    if (!SHADOW) live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
+  }
+  uint32_t nb = 0;                                           // wave-uniform fill of the LDS buffer
+  auto flush = [&]() {
+    __syncthreads();
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(P.count + (SHADOW ? 1 : 0), nb);
+    base = (uint32_t)__shfl((int)base, 0);
+    for (uint32_t q = (uint32_t)lane; q < nb; q += 64)
+      if (base + q < P.cap) { P.key[base + q] = sk[q]; P.val[base + q] = sv[q]; }
+    __syncthreads();
+    nb = 0;
+  };
+  auto emit = [&](bool h, uint32_t ob, uint32_t id) {
+    const uint64_t m = __ballot(h);
+    if (!m) return;
+    const uint32_t c = (uint32_t)__popcll(m);
+    if (nb + c > RT_WFP_BUF) flush();
+    if (h) {
+      const uint32_t q = nb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      sk[q] = ob;
+      sv[q] = id;
+    }
+    nb += c;
+  };
+  auto walk = [&](bool act0, V3 o, V3 dir, double tmax, uint32_t id) {
+    const CullRay cr = cull_ray(o, dir);
+    const RtTrav* __restrict__ TR = S.trav;
+    const int nt = S.n_trav;
+    int t = act0 ? 0 : nt;
+    while (__ballot(t < nt)) {
+      bool h = false;
+      int ob = 0;
+      if (t < nt) {
+        const RtTrav T = TR[t];
+        const bool in = box_may_hit(T.blo, T.bhi, cr, tmax);
+        if (T.obj < 0) {
+          t = in ? t + 1 : T.skip;
+        } else {
+          ++t;
+          ob = T.obj;
+          h = T.cull != RT_CULL_ALWAYS && !(SHADOW && T.shadow_skip) && (T.cull != RT_CULL_BOX || in);
+        }
+      }
+      emit(h, (uint32_t)ob, id);
+    }
+  };
+  if constexpr (!SHADOW) {
+    if (i < n) { P.tmin[j] = RT_WFP_NONE; P.omin[j] = 0x7fffffff; }   // slots outside the frame too
+    // A bound on the nearest hit: the object whose hit spawned the ray, evaluated first (a ray that
+    // refracted into or reflects inside a closed shape meets it again).  The walk then tests boxes
+    // against [0, cull_tmax(bound)] only -- conservative, as nearest_hit's running best is; the
+    // parent's own pair is still emitted by the walk (its box contains the bound's point).
+    double bound = INFINITY;
+    if (d > 0) {
+      const int32_t par = live ? lv.par[j] : -1;
+      const CullRay cr = cull_ray(ro, rd);
+      uint64_t todo = __ballot(live && par >= 0);
+      while (todo) {                     // the children of one shading wave: mostly one parent
+        const int pu = __builtin_amdgcn_readlane(par, (int)__builtin_ctzll(todo));
+        const uint64_t mine = __ballot(live && par == pu);
+        todo &= ~mine;
+        if ((mine >> lane) & 1) bound = wfp_object_nearest(D, pu, ro, rd, cr);
+      }
+    }
+    walk(live, ro, rd, bound < INFINITY ? cull_tmax(bound) : INFINITY, j);
+  } else {
+    const int32_t oi = live ? P.omin[j] : 0x7fffffff;
+    const bool hit = live && oi != 0x7fffffff;
+    V3 p = {0.0, 0.0, 0.0};
+    if (hit) p = {P.px[j], P.py[j], P.pz[j]};                     // wfp_hit_key_kernel
+    for (int k = 0; k < D.n_lights; ++k) {
+      V3 sdir = {0.0, 0.0, 0.0};
+      double tmax = 0.0;
+      const uint32_t s = j * (uint32_t)D.n_lights + (uint32_t)k;
+      if (hit) {
+        cptr<RtLight> lt = &D.lights[k];
+        const V3 l = sub(ld3(lt->p), p);
+        double ll, ill;
+        len_inv(l, &ll, &ill);
+        sdir = scale(l, ill);
+        tmax = cull_tmax(ll);
+        P.kcnt[s] = 0;
+        P.opq[s] = 0;
+      }
+      walk(hit, p, sdir, tmax, s);
+    }
+  }
+  flush();
+}
+
+// One lane per sorted pair: the waves see one object (two at a run boundary): scalarised over the
+// distinct objects of the wave as shade_inputs does, so every scene read is a scalar load.
+__global__ __launch_bounds__(64) void wfp_near_eval_kernel(RtDevScene S, WfArena A, WfPairs P, int d, int y_first,
+                                                           int band_rows, int band_pitch, int n_rows) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t np = min(P.count[0], P.cap);               // pairs of this level's nearest pass (device)
+  const WfLevel lv = wf_level(A, d);
+  const DS D = make_ds(S);
+  for (uint32_t base = blockIdx.x * 64u; base < np; base += gridDim.x * 64u) {   // wave-uniform bounds
+    const uint32_t i = base + (uint32_t)lane;
+    bool live = i < np;
+    uint32_t o = 0xffffffffu, j = 0;
+    V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+    if (live) {
+      o = P.key_s[i];
+      j = P.val_s[i];
+      live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
+    }
+    const CullRay cr = cull_ray(ro, rd);
+    double best = INFINITY;
+    uint64_t todo = __ballot(live);
+    while (todo) {
+      const uint32_t ou = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)__builtin_ctzll(todo));
+      const uint64_t mine = __ballot(live && o == ou);
+      todo &= ~mine;
+      if ((mine >> lane) & 1) best = wfp_object_nearest(D, (int)ou, ro, rd, cr);
+    }
+    if (live) {
+      P.tp[i] = best;
+      if (best < INFINITY) atomicMin(&P.tmin[j], (unsigned long long)__double_as_longlong(best));
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void wfp_near_tie_kernel(WfPairs P) {
+  const uint32_t np = min(P.count[0], P.cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
+    const double t = P.tp[i];
+    if (!(t < INFINITY)) continue;
+    const uint32_t j = P.val_s[i];
+    if ((unsigned long long)__double_as_longlong(t) == P.tmin[j]) atomicMin(&P.omin[j], (int32_t)P.key_s[i]);
+  }
+}
+
+// Per ray of the level, after the nearest-hit folds: the hit point (wf_ray_core's p) and a coherence
+// key for the shadow and shading passes: the hit object above the top `cbits` bits of the Morton code
+// of the hit point's cell (a wave then shades one object -- shade_inputs' waterfall runs once -- and
+// its shadow rays start close together); misses sort last.
+__global__ __launch_bounds__(256) void wfp_hit_key_kernel(RtDevScene S, WfArena A, WfPairs P, int d, uint32_t n,
+                                                          int y_first, int band_rows, int band_pitch, int n_rows,
+                                                          int cbits) {
+  const WfLevel lv = wf_level(A, d);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t j = (d > 0 && A.perm) ? A.perm[i] : i;
+    V3 ro, rd;
+    uint32_t key = (uint32_t)S.n_objects << cbits;
+    if (wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd) && P.omin[j] != 0x7fffffff) {
+      const V3 p = add(ro, scale(rd, __longlong_as_double((long long)P.tmin[j])));
+      P.px[j] = p.x; P.py[j] = p.y; P.pz[j] = p.z;
+      const uint32_t cell = (wf_key(A, p, V3{0.0, 0.0, 0.0}) & 0x07ffffffu) >> (27 - cbits);
+      key = ((uint32_t)P.omin[j] << cbits) | (cbits ? cell : 0u);
+    }
+    P.hkey[i] = key;
+    P.hval[i] = j;
+  }
+}
+
+__global__ __launch_bounds__(64) void wfp_shadow_eval_kernel(RtDevScene S, WfPairs P) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t np = min(P.count[1], P.cap);               // pairs of this level's shadow pass (device)
+  const DS D = make_ds(S);
+  for (uint32_t base = blockIdx.x * 64u; base < np; base += gridDim.x * 64u) {   // wave-uniform bounds
+    const uint32_t i = base + (uint32_t)lane;
+    const bool live = i < np;
+    uint32_t o = 0xffffffffu, s = 0;
+    V3 p = {0.0, 0.0, 0.0}, sdir = {0.0, 0.0, 0.0};
+    double ll = 0.0;
+    if (live) {
+      o = P.key_s[i];
+      s = P.val_s[i];
+      const uint32_t j = s / (uint32_t)S.n_lights, k = s % (uint32_t)S.n_lights;
+      p = {P.px[j], P.py[j], P.pz[j]};
+      const RtLight& lt = S.lights[k];
+      const V3 l = sub(V3{lt.p[0], lt.p[1], lt.p[2]}, p);              // wf_ray_core's light loop
+      double ill;
+      len_inv(l, &ll, &ill);
+      sdir = scale(l, ill);
+    }
+    const CullRay cr = cull_ray(p, sdir);
+    uint32_t cnt = 0;
+    uint64_t todo = __ballot(live);
+    while (todo) {
+      const uint32_t ou = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)__builtin_ctzll(todo));
+      const uint64_t mine = __ballot(live && o == ou);
+      todo &= ~mine;
+      if ((mine >> lane) & 1) cnt = wfp_object_shadow(D, (int)ou, p, sdir, ll, cr);
+    }
+    if (live && cnt) {
+      if (D.objects[o].transparency == 0.0) atomicOr(&P.opq[s], 1u);
+      else atomicAdd(&P.kcnt[s], cnt);
+    }
+  }
+}
+
+template <bool REFR, bool FC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_WF))) void wfp_shade_kernel(
+    RtDevScene S, WfArena A, WfPairs P, int d, uint32_t n, int y_first, int band_rows, int band_pitch, int n_rows,
+    int max_depth) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+  const WfLevel lv = wf_level(A, d);
+  bool live = i < n;
+  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+  uint32_t j = i;
+  int32_t pix = (int32_t)i;
+  if (live) {
+    j = P.hperm[i];                                          // hit-point order (wfp_hit_key_kernel)
+    live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
+    pix = d > 0 ? lv.pix[j] : (int32_t)j;
+  }
+  Col L = {0.0, 0.0, 0.0};
+  double wt = 0.0, wr = 0.0;
+  bool ch_t = false, ch_r = false;
+  V3 p = {0.0, 0.0, 0.0}, dt = {0.0, 0.0, 0.0}, dr = {0.0, 0.0, 0.0};
+  const uint32_t nl = (uint32_t)S.n_lights;
+  const double T = S.shadow_t;
+  if (live)
+    wf_ray_core<REFR, FC>(
+        make_ds(S), ro, rd, d, max_depth,
+        [&](double* t) {
+          const int32_t oi = P.omin[j];
+          if (oi == 0x7fffffff) { *t = INFINITY; return -1; }
+          *t = __longlong_as_double((long long)P.tmin[j]);
+          return (int)oi;
+        },
+        [&](int k, V3, V3, double) {
+          const uint32_t s = j * nl + (uint32_t)k;
+          if (P.opq[s]) return 0.0;
+          double tr = 1.0;                                     // shadow_transparency's product, order-free
+          for (uint32_t c = P.kcnt[s]; c > 0; --c) {
+            tr *= T;
+            if (tr == 0.0) return 0.0;
+          }
+          return tr;
+        },
+        &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr);
+  wf_append(A, lv, d, lane, live, j, pix, L, wt, wr, ch_t, ch_r, p, dt, dr, live ? P.omin[j] : -1);
+}
+
+}  // namespace
+
+using namespace rt;
+
+extern "C" hipError_t rt_wf_bucket_sort(const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
+                                        uint32_t* vals_out, uint32_t n, const uint32_t* n_dev, uint32_t nb, int shift,
+                                        uint32_t* cnt, bool zero_cnt, hipStream_t stream);
+extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                                       const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit,
+                                       hipStream_t stream);
+
+// Pair-path arrays (render_kernels.hip "wavefront pair path"): per ray of a level (R = the larger of
+// the pixel slots and the level capacity) and, grow-only, the pair lists for `need` pairs.
+static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t lcap, size_t need, WfPairs* P) {
+  const size_t nl = (size_t)std::max(1, c->dev.n_lights);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_omin = al(R * 8), o_px = al(o_omin + R * 4), o_k = al(o_px + 3 * R * 8), o_q = al(o_k + R * nl * 4);
+  const size_t o_h = al(o_q + R * nl * 4), rbytes = al(o_h + 4 * R * 4);
+  if (c->wfr_bytes < rbytes) {
+    if (c->wfr) (void)hipFree(c->wfr);
+    c->wfr = nullptr;
+    c->wfr_bytes = 0;
+    RT_HIP(hipMalloc(&c->wfr, rbytes));
+    c->wfr_bytes = rbytes;
+  }
+  if (need > c->wfp_cap || !c->wfp) {
+    // first size: 4 pairs per ray of a full level (fractal.scene needs ~3); a level that emits more
+    // grows it (RT_OPT_WAVEFRONT_CAP 1 % makes the first size tiny: the overflow tests take that path)
+    const size_t cap = std::min<size_t>(0x7fffffc0ull, std::max<size_t>(need + need / 4, 4 * lcap) + 63) & ~(size_t)63;
+    if (need > cap) return fail(RT_ERR_UNSUPPORTED, "wavefront pair list of %zu pairs too large", need);
+    const size_t bytes = al(3 * 16384 + 4 * cap * 4 + cap * 8);
+    if (c->wfp) (void)hipFree(c->wfp);    // waits for launches that may still use it
+    c->wfp = nullptr;
+    c->wfp_bytes = 0;
+    c->wfp_cap = 0;
+    RT_HIP(hipMalloc(&c->wfp, bytes));
+    c->wfp_bytes = bytes;
+    c->wfp_cap = (uint32_t)cap;
+  }
+  uint8_t* r = (uint8_t*)c->wfr;
+  P->tmin = (unsigned long long*)r;
+  P->omin = (int32_t*)(r + o_omin);
+  P->px = (double*)(r + o_px);
+  P->py = P->px + R;
+  P->pz = P->py + R;
+  P->kcnt = (uint32_t*)(r + o_k);
+  P->opq = (uint32_t*)(r + o_q);
+  P->hkey = (uint32_t*)(r + o_h);
+  P->hval = P->hkey + R;
+  P->hkey_s = P->hval + R;
+  P->hperm = P->hkey_s + R;
+  uint8_t* b = (uint8_t*)c->wfp;
+  const size_t cap = c->wfp_cap;
+  P->cap = (uint32_t)cap;
+  P->count = nullptr;                   // set by the caller: the wavefront arena's counter block
+  P->bins = (uint32_t*)b;               // 3 x RT_BS_MAX_BINS words: nearest / hit-point / shadow sorts
+  P->key = (uint32_t*)(b + 3 * 16384);
+  P->val = P->key + cap;
+  P->key_s = P->val + cap;
+  P->val_s = P->key_s + cap;
+  P->tp = (double*)(P->val_s + cap);
+  return RT_OK;
+}
+
+// One level of the wavefront path through the pair path: candidate pairs, sort by object, pair
+// evaluation and the folds, for the nearest hits and then the shadow rays, then the shading pass.
+// The pair counts stay on the device (the sorts and the evaluation kernels read them; their grids
+// are sized for the arena), so a level costs ONE host synchronisation, at its end: it reads the next
+// level's ray count and both pair counts.  A pair count beyond the arena grows it and runs the level
+// again (the level's outputs are recomputed from its rays; level d + 1 is refilled from empty).
+static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int d, uint32_t n, int a0, int a1,
+                     int a2, int a3, int max_depth, bool refr, bool fc, uint32_t* next) {
+  WfPairs P;
+  int rc = wfp_arena(c, st, R, A.cap, 0, &P);
+  if (rc) return rc;
+  P.count = A.count + RT_WFP_COUNT;
+  const dim3 g((n + 63) / 64), b64(64);
+  const uint32_t nobj = (uint32_t)c->dev.n_objects;
+  uint32_t* bins[3] = {P.bins, P.bins + 4096, P.bins + 8192};
+  for (;;) {
+    // grid-stride evaluations: one pass covers ~4 pairs per ray of the level (fractal: ~3), capped at
+    // 8 waves per SIMD -- small levels then launch hundreds, not thousands, of idle workgroups
+    const dim3 ge(std::max<uint32_t>((uint32_t)c->n_cu, std::min<uint32_t>((uint32_t)(((size_t)n * 4 + 63) / 64),
+                                                                          (uint32_t)c->n_cu * 32u)));
+    RT_HIP(hipMemsetAsync(P.count, 0, 8, st));
+    RT_HIP(hipMemsetAsync(P.bins, 0, 3 * 16384, st));        // the three sorts' bucket counters
+    hipLaunchKernelGGL((wfp_cand_kernel<false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+    RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count, nobj, 0, bins[0], false, st));
+    hipLaunchKernelGGL(wfp_near_eval_kernel, ge, b64, 0, st, c->dev, A, P, d, a0, a1, a2, a3);
+    hipLaunchKernelGGL(wfp_near_tie_kernel, dim3(std::min<uint32_t>((P.cap + 255) / 256, 4096)), dim3(256), 0, st, P);
+    // the hit points and their order for the shadow and shading passes: at most 4096 buckets of
+    // (hit object, coarse hit-point cell), unordered within a bucket (a 16^3-cell-only key and the
+    // full 27-bit radix sort measured slower: profiles/r03o_sort_ab.txt, r03w_*)
+    int cbits = 0;
+    while (cbits < 12 && ((nobj + 1u) << (cbits + 1)) <= 4096u) ++cbits;
+    hipLaunchKernelGGL(wfp_hit_key_kernel, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, c->dev,
+                       A, P, d, n, a0, a1, a2, a3, cbits);
+    RT_HIP(rt_wf_bucket_sort(P.hkey, P.hkey_s, P.hval, P.hperm, n, nullptr, (nobj + 1u) << cbits, 0, bins[1], false, st));
+    hipLaunchKernelGGL((wfp_cand_kernel<true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+    RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count + 1, nobj, 0, bins[2], false, st));
+    hipLaunchKernelGGL(wfp_shadow_eval_kernel, ge, b64, 0, st, c->dev, P);
+    if (refr && fc) hipLaunchKernelGGL((wfp_shade_kernel<true, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
+    else if (refr) hipLaunchKernelGGL((wfp_shade_kernel<true, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
+    else if (fc) hipLaunchKernelGGL((wfp_shade_kernel<false, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
+    else hipLaunchKernelGGL((wfp_shade_kernel<false, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
+    RT_HIP(hipGetLastError());
+    uint32_t cb[RT_WFP_COUNT + 2];        // the whole counter block in one copy: level counts, pair counts
+    RT_HIP(hipMemcpyAsync(cb, A.count, sizeof cb, hipMemcpyDeviceToHost, st));
+    RT_HIP(hipStreamSynchronize(st));
+    *next = d < max_depth ? cb[d + 1] : 0u;
+    const uint32_t pc[2] = {cb[RT_WFP_COUNT], cb[RT_WFP_COUNT + 1]};
+    if (pc[0] <= P.cap && pc[1] <= P.cap) return RT_OK;
+    rc = wfp_arena(c, st, R, A.cap, std::max(pc[0], pc[1]), &P);   // grow (synchronises), then this level again
+    if (rc) return rc;
+    P.count = A.count + RT_WFP_COUNT;
+    bins[0] = P.bins; bins[1] = P.bins + 4096; bins[2] = P.bins + 8192;
+    if (d < max_depth) RT_HIP(hipMemsetAsync(A.count + d + 1, 0, 4, st));
+  }
+}
+
+// The wavefront path (wf_*_kernel): level 0 (the pixel slots), then each level the previous one
+// appended to, sorted by coherence key; then the folds, deepest level first; then the overflow
+// fix-up.  The host reads every level's ray count (one stream synchronisation per level) to launch
+// exactly one wave per 64 rays and to stop at the first empty level.
+int rt::launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int a3, int max_depth, uint8_t* target,
+                            size_t tstride, bool f64, int rgbi, size_t n_tiles) {
+  const size_t slots = n_tiles * 64, cap = std::max<size_t>(64, (slots * (size_t)c->wf_cap_pct / 100 + 63) & ~(size_t)63);
+  if (cap > 0x7fffffffull || slots > 0x7fffffffull) return fail(RT_ERR_UNSUPPORTED, "wavefront launch of %zu pixel slots too large", slots);
+  size_t sort_bytes = 0;
+  RT_HIP(rt_wf_sort_pairs(nullptr, &sort_bytes, nullptr, nullptr, nullptr, nullptr, (int)cap, 30, st));
+  const size_t levels = slots * RT_WF_BYTES0 + (size_t)max_depth * cap * RT_WF_BYTES;
+  const size_t o_cnt = (levels + 255) & ~(size_t)255, o_ovf = o_cnt + 256, o_kout = (o_ovf + slots + 255) & ~(size_t)255;
+  const size_t o_perm = o_kout + cap * 4, o_tmp = (o_perm + cap * 4 + 255) & ~(size_t)255, bytes = o_tmp + sort_bytes + 256;
+  if (c->wf_bytes < bytes) {
+    if (c->wf) (void)hipFree(c->wf);          // waits for launches that may still use it
+    c->wf = nullptr;
+    c->wf_bytes = 0;
+    RT_HIP(hipMalloc(&c->wf, bytes));
+    c->wf_bytes = bytes;
+  }
+  uint8_t* base = (uint8_t*)c->wf;
+  WfArena A;
+  A.base = base;
+  A.count = (uint32_t*)(base + o_cnt);
+  A.ovf = base + o_ovf;
+  A.perm = nullptr;
+  A.slots = (uint32_t)slots;
+  A.cap = (uint32_t)cap;
+  for (int k = 0; k < 3; ++k) {
+    A.klo[k] = c->wf_klo[k];
+    A.kscale[k] = 512.0 / std::max(1e-9, c->wf_khi[k] - c->wf_klo[k]);
+  }
+  uint32_t* kout = (uint32_t*)(base + o_kout);
+  uint32_t* perm = (uint32_t*)(base + o_perm);
+  void* tmp = base + o_tmp;
+  RT_HIP(hipMemsetAsync(A.count, 0, 256, st));
+  RT_HIP(hipMemsetAsync(A.ovf, 0, slots, st));
+  const bool refr = c->dev.any_transparent != 0, fc = c->dev.colour_fast != 0 && c->fast_clamp;
+  const bool pairs = c->wf_pairs > 0 && c->dev.shadow_pow != 0 && c->dev.n_objects > 0 && c->dev.n_objects < 4096;
+  auto pairs_level = [&](int d) { return pairs && (d > 0 || c->wf_pairs == 2); };
+  uint32_t n_level[RT_MAX_DEPTH_CAP + 2] = {0};
+  n_level[0] = (uint32_t)slots;
+  int last = 0;
+  for (int d = 0; d <= max_depth; ++d) {
+    const uint32_t n = n_level[d];
+    if (n == 0) break;
+    last = d;
+    A.perm = nullptr;
+    if (d > 0) {                                             // this level's slots in key order
+      const WfLevel L = wf_level(A, d);                      // host-side pointer arithmetic only
+      // The pair path reads a level in slot order: its candidate walks are per lane and its
+      // evaluations run in object order, and the sort measured 0.3-0.6 ms per fractal frame slower
+      // than none (profiles/r03o_sort_ab.txt).
+      if (!pairs_level(d)) {
+        size_t tb = sort_bytes;
+        RT_HIP(rt_wf_sort_pairs(tmp, &tb, L.key, kout, L.val, perm, (int)n, 30, st));
+        A.perm = perm;
+      }
+    }
+    const dim3 g((n + 63) / 64);
+    if (pairs_level(d)) {
+      uint32_t cnt = 0;
+      int rc = wfp_level(c, st, A, std::max(slots, cap), d, n, a0, a1, a2, a3, max_depth, refr, fc, &cnt);
+      if (rc) return rc;
+      if (d < max_depth) n_level[d + 1] = std::min<uint32_t>(cnt, (uint32_t)cap);
+      continue;
+    }
+    else if (refr && fc) hipLaunchKernelGGL((wf_trace_kernel<true, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    else if (refr) hipLaunchKernelGGL((wf_trace_kernel<true, false>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    else if (fc) hipLaunchKernelGGL((wf_trace_kernel<false, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    else hipLaunchKernelGGL((wf_trace_kernel<false, false>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    RT_HIP(hipGetLastError());
+    if (d < max_depth) {
+      uint32_t cnt = 0;
+      RT_HIP(hipMemcpyAsync(&cnt, A.count + d + 1, 4, hipMemcpyDeviceToHost, st));
+      RT_HIP(hipStreamSynchronize(st));
+      n_level[d + 1] = std::min<uint32_t>(cnt, (uint32_t)cap);
+    }
+  }
+  const dim3 bf(256);
+  for (int d = last; d >= 0; --d) {
+    const uint32_t n = n_level[d];
+    const dim3 gf((n + 255) / 256);
+    if (f64 && fc) hipLaunchKernelGGL((wf_fold_kernel<true, true>), gf, bf, 0, st, c->dev, A, d, n, a0, a1, a2, a3, target, tstride, rgbi);
+    else if (f64) hipLaunchKernelGGL((wf_fold_kernel<true, false>), gf, bf, 0, st, c->dev, A, d, n, a0, a1, a2, a3, target, tstride, rgbi);
+    else if (fc) hipLaunchKernelGGL((wf_fold_kernel<false, true>), gf, bf, 0, st, c->dev, A, d, n, a0, a1, a2, a3, target, tstride, rgbi);
+    else hipLaunchKernelGGL((wf_fold_kernel<false, false>), gf, bf, 0, st, c->dev, A, d, n, a0, a1, a2, a3, target, tstride, rgbi);
+  }
+  const dim3 gx((unsigned)c->n_cu * 4u);
+#define RT_WF_FIX(R, F, FCv) hipLaunchKernelGGL((wf_fixup_kernel<R, F, FCv>), gx, dim3(64), 0, st, c->dev, A, a0, a1, a2, a3, max_depth, target, tstride, rgbi)
+  if (refr && f64) { if (fc) RT_WF_FIX(true, true, true); else RT_WF_FIX(true, true, false); }
+  else if (refr) { if (fc) RT_WF_FIX(true, false, true); else RT_WF_FIX(true, false, false); }
+  else if (f64) { if (fc) RT_WF_FIX(false, true, true); else RT_WF_FIX(false, true, false); }
+  else { if (fc) RT_WF_FIX(false, false, true); else RT_WF_FIX(false, false, false); }
+#undef RT_WF_FIX
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}
+

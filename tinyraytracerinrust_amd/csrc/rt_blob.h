@@ -17,12 +17,26 @@
 //  * Textures stay RGBA8 in HBM (the reference holds f64 RGBA, 32 B/texel); the kernel
 //    converts with /255.0 exactly as sceneparser/texture.rs:29-33 does.
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
+#else                                // hipRTC (spec.hip): its runtime header keeps these in a namespace
+using __hip_internal::int32_t;
+using __hip_internal::int64_t;
+using __hip_internal::uint8_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#endif
 
 #define RT_EPSILON 10e-7            /* math.rs:2 */
 #define RT_CULL_COORD_MAX 1e6        /* culling boxes / ray origins beyond this are never culled */
 #define RT_MAX_DEPTH_CAP 16          /* recursion frames kept per lane (max_depth <= 16) */
 #define RT_MAX_LITS 4                /* inline hit-filter literals per leaf */
+
+// Kernel modes (rt_device.h trace, k_rows.hip): the reflection-only megakernel; refraction scenes
+// whose rays form chains (RtDevScene::ray_chains); refraction scenes with ray trees.
+#define RT_MODE_REFL 0
+#define RT_MODE_CHAIN 1
+#define RT_MODE_TREE 2
 
 enum RtNodeKind : int32_t {
   RT_N_SPHERE = 0, RT_N_PLANE = 1, RT_N_CUBE = 2,

@@ -1,0 +1,281 @@
+// rt_ctx.hip -- the device context of the C ABI (include/rt_abi.h): device discovery, context
+// create / free, scene upload (rt::flatten -> one HBM blob, rt_blob.h), options, own-queue streams.
+// Host code only; the kernels and their launches live in k_rows.hip, k_wavefront.hip, k_views.hip.
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "rt_ctx.h"
+
+namespace rt {
+
+bool diag_env(const char* name) {
+#ifdef RT_DIAG_ENV
+  return getenv(name) != nullptr;
+#else
+  (void)name;
+  return false;
+#endif
+}
+
+void drop_order(rt_ctx::OrderSlot& s) {
+  if (s.d_order) (void)hipFree(s.d_order);     // hipFree waits for work that may still read it
+  if (s.d_cost) (void)hipFree(s.d_cost);
+  s = rt_ctx::OrderSlot();
+}
+void drop_orders(rt_ctx* c) {
+  for (auto& s : c->order) drop_order(s);
+}
+
+int ensure_scratch(rt_ctx* c, size_t bytes) {
+  if (c->scratch_bytes >= bytes) return RT_OK;
+  if (c->scratch) (void)hipFree(c->scratch);
+  c->scratch = nullptr;
+  c->scratch_bytes = 0;
+  RT_HIP(hipMalloc(&c->scratch, bytes));
+  c->scratch_bytes = bytes;
+  return RT_OK;
+}
+
+bool is_device_ptr(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+}  // namespace rt
+
+using rt::drop_orders;
+
+template <typename T>
+static size_t put(std::vector<uint8_t>& blob, const std::vector<T>& v) {
+  size_t off = (blob.size() + 255) & ~(size_t)255;
+  blob.resize(off + v.size() * sizeof(T) + 16);
+  if (!v.empty()) memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+  return off;
+}
+
+extern "C" {
+
+int rt_device_count(int* count) {
+  if (!count) return fail(RT_ERR_INVALID, "null output");
+  *count = 0;
+  hipError_t e = hipGetDeviceCount(count);
+  if (e != hipSuccess) { *count = 0; return fail(RT_ERR_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e)); }
+  return RT_OK;
+}
+
+int rt_ctx_create(int device, rt_ctx** out) {
+  if (!out) return fail(RT_ERR_INVALID, "null output");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RT_ERR_DEVICE, "no HIP device available");
+  if (device < 0 || device >= n) return fail(RT_ERR_INVALID, "device %d out of range (%d devices)", device, n);
+  RT_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  RT_HIP(hipGetDeviceProperties(&prop, device));
+  rt_ctx* c = new rt_ctx();
+  c->device = device;
+  c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  memset(&c->dev, 0, sizeof c->dev);
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->tev0) != hipSuccess || hipEventCreate(&c->tev1) != hipSuccess) {
+    delete c;
+    return fail(RT_ERR_DEVICE, "stream/event creation failed");
+  }
+  *out = c;
+  return RT_OK;
+}
+
+int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
+  if (!c || !s) return fail(RT_ERR_INVALID, "null argument");
+  rt::FlatScene f;
+  int rc = rt::flatten(*s, &f);
+  if (rc) return rc;
+  std::vector<uint8_t> blob;
+  size_t o_obj = put(blob, f.objects), o_trav = put(blob, f.trav), o_strav = put(blob, f.strav), o_nodes = put(blob, f.nodes),
+         o_leaves = put(blob, f.leaves);
+  size_t o_prog = put(blob, f.prog), o_lights = put(blob, f.lights), o_tex = put(blob, f.textures);
+  size_t o_texels = put(blob, f.texels);
+  RT_HIP(hipSetDevice(c->device));
+  if (c->d_blob) { (void)hipFree(c->d_blob); c->d_blob = nullptr; }
+  c->uploaded = false;
+  RT_HIP(hipMalloc(&c->d_blob, blob.size()));
+  RT_HIP(hipMemcpy(c->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
+  c->blob_bytes = blob.size();
+  uint8_t* b = (uint8_t*)c->d_blob;
+  RtDevScene& d = c->dev;
+  d.objects = (const RtObject*)(b + o_obj);
+  d.trav = (const RtTrav*)(b + o_trav);
+  d.n_trav = (int32_t)f.trav.size();
+  d.strav = (const RtTrav*)(b + o_strav);
+  d.n_strav = (int32_t)f.strav.size();
+  d.nodes = (const RtNode*)(b + o_nodes);
+  d.leaves = (const RtLeaf*)(b + o_leaves);
+  d.prog = (const RtProg*)(b + o_prog);
+  d.lights = (const RtLight*)(b + o_lights);
+  d.textures = (const RtTexture*)(b + o_tex);
+  d.texels = b + o_texels;
+  d.n_objects = (int32_t)f.objects.size();
+  d.n_lights = (int32_t)f.lights.size();
+  d.n_leaves = (int32_t)f.leaves.size();
+  d.n_nodes = (int32_t)f.nodes.size();
+  d.width = f.width;
+  d.height = f.height;
+  d.any_transparent = f.any_transparent;
+  d.shadow_early_out = f.shadow_early_out;
+  d.colour_fast = f.colour_fast;
+  d.ray_chains = f.ray_chains;
+  d.shadow_pow = f.shadow_pow;
+  d.shadow_t = f.shadow_t;
+  d.cam = f.cam;
+  c->max_depth = f.max_depth;
+  {                                   // the wavefront path's key extent: the hull of the bounded objects
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (const RtObject& o : f.objects)
+      if (o.cull == RT_CULL_BOX)
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], o.blo[k]); hi[k] = std::max(hi[k], o.bhi[k]); }
+    for (int k = 0; k < 3; ++k) {
+      const bool ok = std::isfinite(lo[k]) && std::isfinite(hi[k]) && hi[k] > lo[k];
+      c->wf_klo[k] = ok ? lo[k] : f.cam.center[k] - 100.0;
+      c->wf_khi[k] = ok ? hi[k] : f.cam.center[k] + 100.0;
+    }
+  }
+  c->uploaded = true;
+  drop_orders(c);                     // tile costs belong to the previous scene
+  // the scene-specialised program (spec.hip): the row kernels of the scene's mode; reflection-only
+  // scenes also get the deferred kernels (their tail-bound launches' choice)
+  rt::spec_drop(c);
+  rt::spec_program(f, c);
+  if (c->spec_on) {
+    int rc = rt::spec_build(c);
+    if (rc) return rc;
+  }
+  return RT_OK;
+}
+
+int rt_ctx_kernel_info(rt_ctx* c, char* buf, size_t cap) {
+  if (!c || !buf || cap == 0) return fail(RT_ERR_INVALID, "null argument");
+  char s[256];
+  if (c->spec_mod)
+    snprintf(s, sizeof s, "scene-specialised (hipRTC %016llx, %s, compiled in %.0f ms)%s; last launch: %s",
+             (unsigned long long)c->spec_hash, c->spec_mode == RT_MODE_REFL ? "reflection" : c->spec_mode == RT_MODE_CHAIN ? "chain" : "tree",
+             c->spec_compile_ms, c->spec_compile_ms == 0.0 ? " [process cache]" : "", c->last_kernel);
+  else
+    snprintf(s, sizeof s, "generic (librt_mi355x.so); last launch: %s", c->last_kernel);
+  snprintf(buf, cap, "%s", s);
+  return RT_OK;
+}
+
+int rt_ctx_last_kernel_ms(rt_ctx* c, float* ms) {
+  if (!c || !ms) return fail(RT_ERR_INVALID, "null argument");
+  if (!c->timed) return fail(RT_ERR_INVALID, c->timing ? "no launch recorded" : "RT_OPT_TIMING is off");
+  RT_HIP(hipEventSynchronize(c->ev1));
+  RT_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return RT_OK;
+}
+
+int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
+  if (!c) return fail(RT_ERR_INVALID, "null context");
+  if (option == RT_OPT_TIMING) {
+    if (value != 0 && value != 1) return fail(RT_ERR_INVALID, "RT_OPT_TIMING value %d", value);
+    c->timing = value != 0;
+    c->timed = false;                  // no launch recorded under the new setting yet
+    return RT_OK;
+  }
+  if (option == RT_OPT_SPECIALIZE) {
+    if (value < 0 || value > 2) return fail(RT_ERR_INVALID, "RT_OPT_SPECIALIZE value %d", value);
+    if (value == c->spec_on) return RT_OK;
+    RT_HIP(hipSetDevice(c->device));
+    RT_HIP(hipDeviceSynchronize());             // launches in flight may still run the modules
+    rt::spec_drop(c);
+    c->spec_on = value;
+    return c->uploaded && value ? rt::spec_build(c) : RT_OK;
+  }
+  if (option == RT_OPT_WAVEFRONT_PAIRS) {
+    if (value < 0 || value > 2) return fail(RT_ERR_INVALID, "RT_OPT_WAVEFRONT_PAIRS %d not in [0, 2]", value);
+    c->wf_pairs = value;
+    return RT_OK;
+  }
+  if (option == RT_OPT_WAVEFRONT_CAP) {
+    if (value < 1 || value > 400) return fail(RT_ERR_INVALID, "RT_OPT_WAVEFRONT_CAP %d not in [1, 400]", value);
+    c->wf_cap_pct = value;
+    return RT_OK;
+  }
+  if (option == RT_OPT_TILE_ORDER || option == RT_OPT_FAST_CLAMP) {
+    if (value != 0 && value != 1) return fail(RT_ERR_INVALID, "option %d value %d", option, value);
+    if (option == RT_OPT_FAST_CLAMP) {
+      c->fast_clamp = value != 0;
+    } else if (c->tile_order != (value != 0)) {
+      RT_HIP(hipSetDevice(c->device));
+      drop_orders(c);
+      c->tile_order = value != 0;
+    }
+    return RT_OK;
+  }
+  if (option != RT_OPT_KERNEL) return fail(RT_ERR_INVALID, "unknown option %d", option);
+  if (value != RT_KERNEL_AUTO && value != RT_KERNEL_MEGA && value != RT_KERNEL_DEFERRED && value != RT_KERNEL_WAVEFRONT)
+    return fail(RT_ERR_INVALID, "RT_OPT_KERNEL value %d", value);
+  if (value != c->kernel_opt) {
+    // tile orders were built for one kernel (split entries only for the deferred one): rebuild
+    RT_HIP(hipSetDevice(c->device));
+    drop_orders(c);
+    c->kernel_opt = value;
+  }
+  return RT_OK;
+}
+
+int rt_stream_create(int device, void** stream) {
+  if (!stream) return fail(RT_ERR_INVALID, "null argument");
+  int n_dev = 0;
+  RT_HIP(hipGetDeviceCount(&n_dev));
+  if (device < 0 || device >= n_dev) return fail(RT_ERR_INVALID, "device %d of %d", device, n_dev);
+  RT_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  RT_HIP(hipGetDeviceProperties(&prop, device));
+  // every CU enabled: the mask only buys the stream a hardware queue of its own
+  std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0xFFFFFFFFu);
+  if (prop.multiProcessorCount % 32) mask.back() = (1u << (prop.multiProcessorCount % 32)) - 1u;
+  hipStream_t st = nullptr;
+  RT_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+  *stream = st;
+  return RT_OK;
+}
+
+int rt_stream_destroy(void* stream) {
+  if (!stream) return fail(RT_ERR_INVALID, "null stream");
+  RT_HIP(hipStreamDestroy((hipStream_t)stream));
+  return RT_OK;
+}
+
+int rt_ctx_synchronize(rt_ctx* c) {
+  if (!c) return fail(RT_ERR_INVALID, "null context");
+  RT_HIP(hipSetDevice(c->device));
+  RT_HIP(hipStreamSynchronize(c->stream));
+  return RT_OK;
+}
+
+void rt_ctx_free(rt_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (c->d_blob) (void)hipFree(c->d_blob);
+  if (c->scratch) (void)hipFree(c->scratch);
+  if (c->wf) (void)hipFree(c->wf);
+  if (c->wfr) (void)hipFree(c->wfr);
+  if (c->wfp) (void)hipFree(c->wfp);
+  drop_orders(c);
+  rt::spec_drop(c);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->tev0) (void)hipEventDestroy(c->tev0);
+  if (c->tev1) (void)hipEventDestroy(c->tev1);
+  delete c;
+}
+
+}  // extern "C"

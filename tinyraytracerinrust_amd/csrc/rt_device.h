@@ -1,0 +1,1338 @@
+// rt_device.h -- the gfx950 (MI355X, CDNA4) device core of the TinyRaytracer render path: the
+// reference's per-ray algorithm (get_ray_color and everything it calls) as device functions, shared
+// by every kernel translation unit (k_rows.hip, k_wavefront.hip, k_views.hip) and by the
+// scene-specialised kernel that hipRTC compiles at scene upload (k_spec.hip, RT_SPEC below).
+//
+// One thread per pixel; each 64-lane wave owns an 8x8 pixel tile (coherent primary rays,
+// fewer divergent CSG/shade branches than a 64x1 row strip).  All arithmetic is IEEE f64 with NO
+// contraction (Rust never fuses): every TU is compiled with -ffp-contract=off and the pragma
+// below.  sqrt and division lower to correctly rounded sequences on gfx950 (verified bit-exact
+// against glibc, profiles/r01_libm_probe.txt); acos is rt_acos (rt_math.h: 1 ulp from glibc on
+// ~0.4% of inputs, and far fewer registers than ocml's); sin comes from ocml and may differ from
+// glibc by 1 ulp (DESIGN.md "Parity").
+//
+// The reference's recursion (get_ray_color calling itself for refraction and reflection,
+// raytracer.rs:242-280) becomes an explicit per-lane frame stack combined in the same
+// post-order: child colour C folds into its parent as in_range(A + in_range(C * w)) where
+// A = parent.intensify(1 - w) -- exactly the `final.intensify(1-w) + R.intensify(w)` of
+// raytracer.rs:256-257 / :278-279.
+#pragma once
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include "../../include/rt_abi.h"
+#else                                // hipRTC (spec.hip): no libc headers
+#define INFINITY __builtin_inf()
+using __hip_internal::size_t;
+#endif
+
+#define RT_HD __device__
+#include "rt_blob.h"
+// Correctly rounded sqrt(x) and 1/sqrt-derived reciprocals without their range handling.
+// For f64 `sqrt` and `/` the compiler emits (gfx950) scaled Newton sequences:
+//   sqrt(x): x scaled by 2^256 if x < 2^-767, y = rsq(x), g = x*y, h = 0.5*y, r = fma(-h,g,0.5),
+//            g = fma(g,r,g), h = fma(h,r,h), twice {d = fma(-g,g,x), g = fma(d,h,g)}, g scaled back,
+//            and x itself returned for +-0 / +inf (17 VALU instructions);
+//   a / b:   v_div_scale of b and of a, rcp, 4 Newton fmas, mul, fma, v_div_fmas, v_div_fixup (11).
+// For x in [2^-767, DBL_MAX] the scalings are by 2^0 and the class select returns g, so the
+// unscaled core below is the SAME operation sequence on the same values: bit-identical.  Then
+// l = sqrt(x) is in [2^-383.5, 2^512): for 1.0 / l v_div_scale scales neither operand (both
+// normal, exponent gap < 768, 1/l and the quotient normal), so v_div_fmas is a plain fma (VCC 0),
+// the mul by the numerator 1.0 is exact, and v_div_fixup returns its positive normal operand:
+// again the same values.  The range test is wave-uniform (one ballot), outside it the compiler's
+// sequences run.  RT_FAST_SQRT=0 restores the plain `sqrt` / `/` everywhere.
+#ifndef RT_FAST_SQRT
+#define RT_FAST_SQRT 1
+#endif
+static __device__ __forceinline__ double sqrt_core(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
+static __device__ __forceinline__ double recip_core(double l) {     // 1.0 / l for l in [2^-384, 2^512]
+  const double nl = -l;
+  const double r = __builtin_amdgcn_rcp(l);
+  const double f0 = __builtin_fma(nl, r, 1.0);
+  const double f1 = __builtin_fma(r, f0, r);
+  const double f2 = __builtin_fma(nl, f1, 1.0);
+  const double f3 = __builtin_fma(f1, f2, f1);
+  const double f4 = __builtin_fma(nl, f3, 1.0);            // mul = 1.0 * f3 = f3
+  return __builtin_fma(f4, f3, f3);
+}
+// a / b when neither v_div_scale scales (both operands normal, exponent gap < 768, quotient
+// normal, |a| >= 2^-969) or a == 0: the compiler's sequence with those identities dropped;
+// v_div_fixup is kept, so a zero numerator gives the same signed zero.
+static __device__ __forceinline__ double div_core(double a, double b) {
+  const double nb = -b;
+  const double r = __builtin_amdgcn_rcp(b);
+  const double f0 = __builtin_fma(nb, r, 1.0);
+  const double f1 = __builtin_fma(r, f0, r);
+  const double f2 = __builtin_fma(nb, f1, 1.0);
+  const double f3 = __builtin_fma(f1, f2, f1);
+  const double m = a * f3;
+  const double f4 = __builtin_fma(nb, m, a);
+  return __builtin_amdgcn_div_fixup(__builtin_fma(f4, f3, m), b, a);
+}
+// rt_math.h's rt_acos takes these for the operations whose operand ranges it guarantees.
+#ifndef RT_ACOS_CORES
+#define RT_ACOS_CORES 1
+#endif
+#if RT_FAST_SQRT && RT_ACOS_CORES
+#define RT_SQRT_IN_RANGE(x) sqrt_core(x)
+#define RT_DIV_IN_RANGE(a, b) div_core(a, b)
+#endif
+#include "rt_math.h"
+
+#pragma clang fp contract(off)
+
+// The device functions below are inlined into every kernel.  In the specialised program (RT_SPEC,
+// one module holding 8 kernels of one scene) the inliner would otherwise keep the big ones as
+// calls (14 s_swappc, the call ABI's saves and scratch); every kernel instantiates its own copy.
+#ifdef RT_SPEC
+// A value the optimiser must treat as computed here: trace()'s light loop calls the shadow walk with
+// the same origin for every light, and with every box and transform a constant the walk's terms on
+// the origin ((lo - o), xf(inv, o)) become loop-invariant -- LICM then hoists those of EVERY box and
+// leaf out of the light loop and the spec kernel spills ~200 VGPRs.  Re-defining the origin at the
+// walk keeps each term where the generic kernel computes it (no instruction, no value change).
+#define RT_OPAQUE(x) asm volatile("" : "+v"(x))
+#define RT_FN __device__ __attribute__((always_inline))
+#define RT_SPEC_UNROLL _Pragma("unroll")   // loops over a constant record's runs: unroll them fully
+#else
+#define RT_OPAQUE(x) (void)0
+#define RT_FN __device__
+#define RT_SPEC_UNROLL
+#endif
+
+namespace {
+
+// Scene tables are read-only for the whole launch: view them through the CONSTANT address space
+// (4) so uniform-index reads compile to scalar (SMEM) loads instead of per-lane VMEM loads.
+#define CAS __attribute__((address_space(4)))
+template <class T> using cptr = const CAS T*;
+template <class T> __device__ __forceinline__ cptr<T> as_const(const T* p) { return (cptr<T>)p; }
+
+struct DS {                         // device view of RtDevScene
+  cptr<RtObject> objects;
+  cptr<RtTrav> trav;
+  cptr<RtTrav> strav;               // shadow-ray walk of scenes without a transparent object
+  cptr<RtNode> nodes;
+  cptr<RtLeaf> leaves;
+  cptr<RtProg> prog;
+  cptr<RtLight> lights;
+  cptr<RtTexture> textures;
+  const uint8_t* texels;            // per-lane texel gathers stay global (vector) loads
+  int n_objects, n_lights, n_trav, n_strav;
+  int shadow_early_out;
+};
+
+constexpr double EPS = RT_EPSILON;
+#ifndef RT_PLANE_AXIS
+#define RT_PLANE_AXIS 1             // axis-aligned planes: one product per dot in the traversals
+#endif
+#ifndef RT_NEAREST_ORDER
+#define RT_NEAREST_ORDER 1          // reflection-only kernels: nearest-hit walk in the shadow walk's order (tie-exact)
+#endif
+#ifndef RT_SHADOW_ORDER
+#define RT_SHADOW_ORDER 1           // reflection-only kernels: shadow rays walk the likeliest occluders first
+#endif
+#ifndef RT_CONST_FILTER
+#define RT_CONST_FILTER 1           // skip hit filters the host proved constant (RtLeaf::filter_const) in the
+                                    // refraction kernels (SHARE): spinning_globes' glass shells, 10.5 % faster;
+                                    // in the reflection-only megakernel the test cost 4 more spilled VGPRs
+                                    // (profiles/r02co_const_filter_ab.txt)
+#endif
+#ifndef RT_SPHERE_SHARE
+#define RT_SPHERE_SHARE 1           // concentric sphere leaves with one transform share their ray terms
+#endif
+#ifndef RT_SPHERE_SHARE_CHAIN
+#define RT_SPHERE_SHARE_CHAIN 1     // the refraction-chain kernel shares sphere terms too
+#endif
+constexpr double PI_D = 3.14159265358979323846;   // std::f64::consts::PI
+
+struct V3 { double x, y, z; };
+struct Col { double r, g, b; };
+
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V3 scale(V3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ bool wave_sqrt_core_ok(double x) {
+  return __ballot(!(x >= 0x1p-767 && x <= 0x1.fffffffffffffp+1023)) == 0;
+}
+__device__ __forceinline__ double sqrt_rt(double x) {
+#if RT_FAST_SQRT
+  if (wave_sqrt_core_ok(x)) return sqrt_core(x);
+#endif
+  return sqrt(x);
+}
+__device__ __forceinline__ double len(V3 a) { return sqrt_rt(dot(a, a)); }
+// l = len(a) and il = 1.0 / l, as `len(a)` and `1.0 / len(a)` compute them
+__device__ __forceinline__ void len_inv(V3 a, double* l, double* il) {
+  const double x = dot(a, a);
+#if RT_FAST_SQRT
+  if (wave_sqrt_core_ok(x)) {
+    *l = sqrt_core(x);
+    *il = recip_core(*l);
+    return;
+  }
+#endif
+  *l = sqrt(x);
+  *il = 1.0 / *l;
+}
+__device__ __forceinline__ V3 normalized(V3 a) {
+  double l, il;
+  len_inv(a, &l, &il);
+  return scale(a, il);
+}
+template <class P> __device__ __forceinline__ V3 ld3(P p) { return {p[0], p[1], p[2]}; }
+// transform_vector (transformation.rs:53-59) with rows m[0..3], m[4..7], m[8..11]
+template <class P> __device__ __forceinline__ V3 xf(P m, V3 v) {
+  return {m[0] * v.x + m[1] * v.y + m[2] * v.z + m[3],
+          m[4] * v.x + m[5] * v.y + m[6] * v.z + m[7],
+          m[8] * v.x + m[9] * v.y + m[10] * v.z + m[11]};
+}
+// transform_vector by a diagonal-affine matrix (RtLeaf::xdiag): bit-identical to xf() for finite
+// inputs (rt_blob.h), 6 flops instead of 18.
+template <class P> __device__ __forceinline__ V3 xf_diag(P m, V3 v) {
+  return {m[0] * v.x + m[3], m[5] * v.y + m[7], m[10] * v.z + m[11]};
+}
+__device__ __forceinline__ bool finite3(V3 v) { return isfinite(v.x) && isfinite(v.y) && isfinite(v.z); }
+// Is every active lane's vector finite?  Wave-uniform, so the short transform is a scalar branch.
+__device__ __forceinline__ bool wave_finite(V3 a) { return __ballot(!finite3(a)) == 0; }
+__device__ __forceinline__ bool wave_finite(V3 a, V3 b) { return __ballot(!(finite3(a) && finite3(b))) == 0; }
+// The leaf's inverse transform of a point (transformation.rs:53-59); `fin` = wave_finite(v).
+__device__ __forceinline__ V3 leaf_inv_xf(cptr<RtLeaf> L, V3 v, bool fin) {
+  if (L->xdiag == RT_XF_IDENTITY && fin) return v;
+  if (L->xdiag && fin) return xf_diag(L->inv, v);
+  return xf(L->inv, v);
+}
+
+// color.rs:36-53: clamp each channel (NaN passes through)
+// FC (fast clamp): the same clamp as two min/max instructions instead of two compares and four
+// selects.  fmin(fmax(x, 0), 1) equals `x < 0 ? 0 : (x > 1 ? 1 : x)` bit for bit for every x
+// except NaN (maxNum drops it) and -0 (max(-0, +0) is +0).  The host sets RtDevScene::colour_fast
+// only when no colour-op operand can be NaN, negative or -0 (every material / light colour channel
+// finite and >= +0, every reflectivity and transparency finite in [0, 1]: then every factor of
+// every colour op is finite and >= +0, see rt::flatten), and the kernels take FC = true only then.
+// 3.4 % faster on 4K globes, 2 % on spinning_globes (profiles/r02ab.txt).
+template <bool FC = false> __device__ __forceinline__ double in_limit(double x) {
+  if constexpr (FC) return __builtin_fmin(__builtin_fmax(x, 0.0), 1.0);
+  else return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x);
+}
+template <bool FC = false> __device__ __forceinline__ Col in_range(double r, double g, double b) {
+  return {in_limit<FC>(r), in_limit<FC>(g), in_limit<FC>(b)};
+}
+template <bool FC = false> __device__ __forceinline__ Col intensify(Col c, double k) { return in_range<FC>(c.r * k, c.g * k, c.b * k); }
+template <bool FC = false> __device__ __forceinline__ Col cmul(Col a, Col b) { return in_range<FC>(a.r * b.r, a.g * b.g, a.b * b.b); }
+template <bool FC = false> __device__ __forceinline__ Col cadd(Col a, Col b) { return in_range<FC>(a.r + b.r, a.g + b.g, a.b + b.b); }
+// `(c * 255.0) as u8` (easy_pixbuf.rs:49-52): saturating truncation, NaN -> 0
+__device__ __forceinline__ uint32_t to_u8(double c) {
+  double v = c * 255.0;
+  if (!(v > 0.0)) return 0u;
+  if (v >= 255.0) return 255u;
+  return (uint32_t)v;
+}
+
+// ------------------------------------------------------------------ primitives (math_shapes.rs)
+template <class P> __device__ __forceinline__ bool on_plane(P pl, V3 q) {        // :162-164
+  return fabs(pl[0] * q.x + pl[1] * q.y + pl[2] * q.z + pl[3]) < EPS;
+}
+
+RT_FN bool leaf_inside(cptr<RtLeaf> L, V3 p, bool fin) {
+  int k = L->kind;
+  if (k == RT_N_PLANE) return false;                                        // :186-188
+  V3 q = leaf_inv_xf(L, p, fin);
+  if (k == RT_N_SPHERE) return len(sub(q, ld3(L->c))) <= L->r_eps;         // :70-74
+  return q.x <= L->hi[0] && q.x >= L->lo[0] && q.y <= L->hi[1] &&          // :319-328
+         q.y >= L->lo[1] && q.z <= L->hi[2] && q.z >= L->lo[2];
+}
+
+RT_FN bool leaf_on_surface(cptr<RtLeaf> L, V3 p, bool fin) {
+  V3 q = leaf_inv_xf(L, p, fin);
+  int k = L->kind;
+  if (k == RT_N_SPHERE) return fabs(len(sub(q, ld3(L->c))) - L->radius) < EPS;   // :76-80
+  if (k == RT_N_PLANE) return on_plane(L->pl[0], q);                            // :190-194
+  bool bx = L->lo_e[0] <= q.x && q.x <= L->hi_e[0];                              // :330-355
+  bool by = L->lo_e[1] <= q.y && q.y <= L->hi_e[1];
+  bool bz = L->lo_e[2] <= q.z && q.z <= L->hi_e[2];
+  if (by && bx && (on_plane(L->pl[0], q) || on_plane(L->pl[5], q))) return true;
+  if (bz && bx && (on_plane(L->pl[1], q) || on_plane(L->pl[4], q))) return true;
+  if (by && bz && (on_plane(L->pl[2], q) || on_plane(L->pl[3], q))) return true;
+  return false;
+}
+
+RT_FN V3 leaf_normal(cptr<RtLeaf> L, V3 p, bool fin) {
+  int k = L->kind;
+  if (k == RT_N_PLANE) return ld3(L->pn[0]);                               // :182-184
+  V3 q = leaf_inv_xf(L, p, fin);
+  if (k == RT_N_SPHERE) {                                                  // :64-68
+    V3 n = sub(q, ld3(L->c));
+    return normalized(sub(xf(L->mat, n), ld3(L->mat_o)));
+  }
+  RT_SPEC_UNROLL
+  for (int i = 0; i < 6; ++i)                                              // :292-317
+    if (on_plane(L->pl[i], q)) return ld3(L->pn[i]);
+  return {1.0, 1.0, 1.0};
+}
+
+// MathSphere::get_uv_coordinates (:82-114): the centre is subtracted BEFORE the inverse transform
+RT_FN void sphere_uv(cptr<RtLeaf> L, V3 p, double* u, double* v) {
+  V3 q = xf(L->inv, sub(p, ld3(L->c)));           // per shaded hit only: no short form
+  q = scale(normalized(q), 1.0 - EPS);
+  double phi = rt_acos(-((0.0 * q.x + 1.0 * q.y) + 0.0 * q.z));             // up = (0,1,0)
+  if (isnan(phi)) phi = 0.0;
+  double theta = (rt_acos(((q.x * 0.0 + q.y * 0.0) + q.z * -1.0) / sin(phi))) / (2.0 * PI_D);   // u_zero = (0,0,-1)
+  if (isnan(theta)) theta = 0.0;
+  *v = phi / PI_D;
+  *u = ((-1.0 * q.x + 0.0 * q.y) + 0.0 * q.z > 0.0) ? 1.0 - theta : theta;  // u_qrtr = (-1,0,0)
+}
+
+// Candidate hit distances of one primitive for the world ray (ro, rd):
+// RTObject::intersects (rt_object.rs:28-31) = reverse_transform_ray + MathShape::intersects.
+// `fin` = wave_finite(ro, rd): selects the exact short forms for identity / diagonal-affine
+// leaves (rt_blob.h).  POS: the caller accepts only t > EPS (the traversals), so a plane whose
+// distance is provably <= 0 from the signs alone skips its division (see the plane branch).
+// SphereShare: a traversal's per-lane record of the last sphere leaf's ray terms.  A sphere leaf
+// with RtLeaf::share_prev (the previous leaf of its object is a sphere with a bit-identical
+// inverse transform and centre, and is evaluated by every lane that evaluates this one, see
+// rt_blob.h) has the same object-space ray, hence the same 1/|d|, v.dn and v.v: only r^2 differs,
+// so it reuses them and skips the transform, the length, the division and two dot products.
+struct SphereShare { double il, vd, vv; };
+
+template <bool POS = false>
+__device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, bool fin, double* t0, double* t1,
+                                               SphereShare* sh = nullptr) {
+#if RT_SPHERE_SHARE
+  if (sh && L->share_prev) {                                               // math_shapes.rs:42-62
+    const double sum = sh->vd * sh->vd - (sh->vv - L->r2);
+    if (sum < 0.0) return 0;
+    const double sq = sqrt_rt(sum);
+    *t0 = (-sh->vd + sq) * sh->il;
+    *t1 = (-sh->vd - sq) * sh->il;
+    return 2;
+  }
+#endif
+  V3 o, d;
+  if (L->xdiag == RT_XF_IDENTITY && fin) {
+    o = ro;
+    d = rd;
+  } else if (L->xdiag && fin) {                                            // transformation.rs:88-93
+    o = xf_diag(L->inv, ro);
+    d = sub(xf_diag(L->inv, rd), ld3(L->inv_o));
+  } else {
+    o = xf(L->inv, ro);
+    d = sub(xf(L->inv, rd), ld3(L->inv_o));
+  }
+  int k = L->kind;
+  if (k == RT_N_SPHERE) {                                                  // math_shapes.rs:42-62
+    V3 v = sub(o, ld3(L->c));
+    double l, il;
+    len_inv(d, &l, &il);                                                   // il = 1.0 / len(d)
+    V3 dn = scale(d, il);
+    double vd = dot(v, dn);
+    const double vv = dot(v, v);
+    if (sh) *sh = {il, vd, vv};
+    double sum = vd * vd - (vv - L->r2);
+    if (sum < 0.0) return 0;
+    double sq = sqrt_rt(sum);
+    *t0 = (-vd + sq) * il;
+    *t1 = (-vd - sq) * il;
+    return 2;
+  }
+  if (k == RT_N_PLANE) {                                                   // :168-180
+    V3 pn = ld3(L->pnorm);
+    double v_d, num;
+#if RT_PLANE_AXIS
+    const int ax = L->plane_axis;
+    if (POS && fin && ax >= 0) {               // axis-aligned normal: one product (rt_blob.h)
+      if (ax == 0) { v_d = pn.x * d.x; num = pn.x * o.x; }
+      else if (ax == 1) { v_d = pn.y * d.y; num = pn.y * o.y; }
+      else { v_d = pn.z * d.z; num = pn.z * o.z; }
+    } else
+#endif
+    {
+      v_d = dot(pn, d);
+      num = dot(pn, o);
+    }
+    if (v_d != 0.0) {
+      num = num + L->pl[0][3];
+      // t = -num * (1/v_d) is > 0 only if num and v_d have opposite signs (rounding keeps signs;
+      // 1/v_d may overflow to +-inf, never to 0).  Otherwise t is <= 0, -0 or NaN: never > EPS.
+      if (POS && !((num > 0.0 && v_d < 0.0) || (num < 0.0 && v_d > 0.0))) return 0;
+      double t = -num * (1.0 / v_d);
+      if (t >= 0.0) { *t0 = t; return 1; }
+    }
+    return 0;
+  }
+  double tn = -INFINITY, tf = INFINITY;                                    // :248-290
+#define RT_SLAB(P, D, I)                                                    \
+  if (D == 0.0) {                                                           \
+    if (P < L->lo[I] || P > L->hi[I]) return 0;                             \
+  } else {                                                                  \
+    double a = (L->lo[I] - P) / D, b = (L->hi[I] - P) / D;                  \
+    if (a > b) { double tmp = a; a = b; b = tmp; }                          \
+    if (a > tn) tn = a;                                                     \
+    if (b < tf) tf = b;                                                     \
+    if (tn > tf || tf < 0.0) return 0;                                      \
+  }
+  RT_SLAB(o.x, d.x, 0)
+  RT_SLAB(o.y, d.y, 1)
+  RT_SLAB(o.z, d.z, 2)
+#undef RT_SLAB
+  *t0 = tn;
+  *t1 = tf;
+  return 2;
+}
+
+// Conjunction of every CSG ancestor's sibling test for a hit of leaf L at world point p
+// (csg.rs:43-95), as a postfix program over a bit stack.
+RT_FN bool leaf_filter(const DS& S, cptr<RtLeaf> L, V3 p) {
+  const bool fin = wave_finite(p);
+  const int nl = L->n_lit;
+  if (nl >= 0) {                                   // conjunction of literals (rt_blob.h)
+    RT_SPEC_UNROLL
+    for (int k = 0; k < nl; ++k) {
+      const int v = L->lit[k];
+      if (leaf_inside(&S.leaves[v >> 1], p, fin) != (bool)(v & 1)) return false;
+    }
+    return true;
+  }
+  uint32_t st = 0;
+  const int e = L->prog_end;
+  RT_SPEC_UNROLL
+  for (int k = L->prog_begin; k < e; ++k) {
+    const int op = S.prog[k].op, arg = S.prog[k].arg;
+    if (op == RT_OP_INSIDE) {
+      st = (st << 1) | (leaf_inside(&S.leaves[arg], p, fin) ? 1u : 0u);
+    } else if (op == RT_OP_REQUIRE) {
+      uint32_t v = st & 1u;
+      st >>= 1;
+      if (v != (uint32_t)arg) return false;
+    } else {
+      uint32_t b = st & 1u;
+      st >>= 1;
+      uint32_t a = st & 1u, r;
+      if (op == RT_OP_AND) r = a & b;
+      else if (op == RT_OP_OR) r = a | b;
+      else r = a & (b ^ 1u);
+      st = (st & ~1u) | r;
+    }
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ conservative culling
+// Does the ray segment t in [0, tmax] come near the box?  Only ever answers "no" when no point
+// where an accepted hit could lie is on the segment.  Per axis the slab times are
+// (bound - o) * inv with inv ~ 1/d to ~1e-15: for |origin|, |bounds| <= 1e6 the error in
+// space is < 1e-9, far inside the 1e-6 inflation of every box (scene.cpp leaf_box), so each
+// axis interval computed still contains the parameter of any point of the un-inflated region;
+// tmax carries a 1e-7 relative margin on top.  min/max are IEEE minNum/maxNum: a NaN slab time
+// narrows nothing, and a ray outside the proven range (cull_ray) gets NaN inv -> never culled.
+struct CullRay { V3 inv, o; };
+
+// Reciprocal for the culling slabs only (never for a value the reference computes): hardware
+// rcp + one Newton step.  d == 0 (or |d| < 1e-200) -> +-1e200, which makes the slab test the
+// "origin inside the slab" check while every product stays finite.
+__device__ __forceinline__ double cull_rcp(double x) {
+  const double r = __builtin_amdgcn_rcp(x);
+  const double n = fma(r, fma(-x, r, 1.0), r);
+  return fabs(x) < 1e-200 ? copysign(1e200, x) : n;
+}
+__device__ __forceinline__ CullRay cull_ray(V3 o, V3 d) {
+  const double ad = fmax(fmax(fabs(d.x), fabs(d.y)), fabs(d.z));
+  const bool ok = fabs(o.x) <= RT_CULL_COORD_MAX && fabs(o.y) <= RT_CULL_COORD_MAX && fabs(o.z) <= RT_CULL_COORD_MAX &&
+                  ad >= 1e-100 && ad <= 1e100;
+  const double nan = __builtin_nan("");
+  const V3 inv = ok ? V3{cull_rcp(d.x), cull_rcp(d.y), cull_rcp(d.z)} : V3{nan, nan, nan};
+  return {inv, o};
+}
+// (bound - o) * inv per slab: measured faster than fma(bound, inv, -o*inv), which keeps three
+// more doubles live across the traversal (profiles/r01n_variant_timing.txt).
+template <class P> __device__ __forceinline__ bool box_may_hit(P lo, P hi, const CullRay& r, double tmax) {
+  const double ax = (lo[0] - r.o.x) * r.inv.x, bx = (hi[0] - r.o.x) * r.inv.x;
+  const double ay = (lo[1] - r.o.y) * r.inv.y, by = (hi[1] - r.o.y) * r.inv.y;
+  const double az = (lo[2] - r.o.z) * r.inv.z, bz = (hi[2] - r.o.z) * r.inv.z;
+  const double tn = fmax(fmax(fmin(ax, bx), fmin(ay, by)), fmax(fmin(az, bz), 0.0));
+  const double tf = fmin(fmin(fmax(ax, bx), fmax(ay, by)), fmin(fmax(az, bz), tmax));
+  return !(tn > tf);
+}
+__device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) + 1e-7; }
+
+// The object's oriented box (RtObject::obb_leaf, scene.cpp obb): may the segment t in [0, tmax]
+// meet the leaf-frame box olo/ohi?  The ray is taken to the leaf's frame with the leaves' own
+// arithmetic; outside the range the host's margins are proven for (|o| <= 1e6, unit-length
+// directions) the answer is yes.  The refraction kernels (SHARE: 4 waves/SIMD at 115-119 VGPRs)
+// do not take it: the test's code alone made spinning_globes (no oriented box) 2.7 % slower
+// (profiles/r02cg_obb_ab.txt).
+#ifndef RT_OBB
+#define RT_OBB 1
+#endif
+__device__ __forceinline__ bool obb_may_hit(const DS& S, cptr<RtObject> O, V3 ro, V3 rd, double tmax) {
+  cptr<RtLeaf> R = &S.leaves[O->obb_leaf];
+  const double ad = fmax(fmax(fabs(rd.x), fabs(rd.y)), fabs(rd.z));
+  if (!(ad >= 0.25 && ad <= 4.0 && fabs(ro.x) <= 1e6 && fabs(ro.y) <= 1e6 && fabs(ro.z) <= 1e6)) return true;
+  const V3 o = xf(R->inv, ro);
+  const V3 d = sub(xf(R->inv, rd), ld3(R->inv_o));
+  return box_may_hit(O->olo, O->ohi, cull_ray(o, d), tmax);
+}
+
+// ------------------------------------------------------------------ traversal (raytracer.rs)
+// Both traversals walk the object hierarchy (RtTrav, pre-order over contiguous draw-order runs)
+// wave-coherently: `i` is uniform, a lane that misses a group resumes at its skip index, and the
+// wave jumps over a group no lane entered.  walk_trav calls group(T) for a group node (does this
+// lane enter it?) and object(T) for an object node the lane reaches.
+// RT_SPEC (the scene-specialised kernel, k_spec.hip): the hierarchy is a constexpr table, so the
+// walk is unrolled at compile time into nested branches -- every node's fields, every object's and
+// leaf's record are constants, and a branch no lane takes is jumped over by the hardware (EXEC = 0),
+// exactly the generic walk's skip.
+#ifdef RT_SPEC
+#define RT_INL __attribute__((always_inline))
+template <int N> struct IC { static constexpr int value = N; };
+template <int I, int END, class F>
+__device__ __forceinline__ void spec_for(F&& f) {
+  if constexpr (I < END) {
+    f(IC<I>{});
+    spec_for<I + 1, END>(f);
+  }
+}
+template <bool SORD, int I, int END, class G, class O>
+__device__ __forceinline__ void spec_walk(G& group, O& object) {
+  if constexpr (I < END) {
+    constexpr RtTrav T = SORD ? rt_spec::STRAV[I] : rt_spec::TRAV[I];
+    cptr<RtTrav> TP = as_const(SORD ? &rt_spec::STRAV[I] : &rt_spec::TRAV[I]);
+    if constexpr (T.obj < 0) {
+      if (group(TP)) spec_walk<SORD, I + 1, T.skip>(group, object);
+      spec_walk<SORD, T.skip, END>(group, object);
+    } else {
+      object(TP);
+      spec_walk<SORD, I + 1, END>(group, object);
+    }
+  }
+}
+#else
+#define RT_INL
+#endif
+// STOP (the shadow walk's early-out): stop(T) after an object node says whether this lane is done;
+// once no lane walks on, the generic walk ends (the spec walk's remaining branches are skipped by
+// the hardware, EXEC = 0).
+template <bool SORD, bool STOP = false, class G, class O>
+__device__ __forceinline__ void walk_trav(const DS& S, G&& group, O&& object, bool* done = nullptr) {
+#ifdef RT_SPEC
+  spec_walk<SORD, 0, SORD ? rt_spec::N_STRAV : rt_spec::N_TRAV>(group, object);
+#else
+  const cptr<RtTrav> TR = SORD ? S.strav : S.trav;
+  const int n_tr = SORD ? S.n_strav : S.n_trav;
+  int resume = 0;
+  for (int i = 0; i < n_tr;) {
+    cptr<RtTrav> T = &TR[i];
+    const bool act = i >= resume;
+    if (T->obj < 0) {                                    // group node
+      const bool in = act && group(T);
+      if (act && !in) resume = T->skip;
+      i = __ballot(in) ? i + 1 : T->skip;
+      continue;
+    }
+    ++i;
+    if (act) object(T);
+    if constexpr (STOP)
+      if (__ballot(!*done) == 0) break;
+  }
+#endif
+}
+
+// Nearest hit over all objects in draw order: accept d if d > EPS && d < nearest
+// (raytracer.rs:141-150).  The acceptance test is pure, so it runs BEFORE the (pure) CSG
+// filter: candidates that cannot win never pay for the sibling is_inside tests.
+// SHARE: concentric sphere leaves reuse their ray terms (SphereShare); it keeps three doubles live
+// across the leaf loop, so only kernels with register headroom take it (see trace()).
+template <bool SHARE = false, bool OBB = !SHARE>
+RT_FN int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist) {
+  double best = INFINITY;
+  int bobj = -1;
+  SphereShare shr = {0.0, 0.0, 0.0};
+  const CullRay cr = cull_ray(ro, rd);
+  const bool fin = wave_finite(ro, rd);
+  // NORDER (reflection-only kernels): the objects in S.strav's order, largest regions first, so an
+  // early hit on a big object culls what lies behind it.  Exact: a candidate equal to the best
+  // distance so far wins when its object comes earlier in DRAW order (o < bobj), which is the
+  // reference's first-visited-wins rule (raytracer.rs:141-150) for any visiting order.
+  constexpr bool NORDER = RT_NEAREST_ORDER && OBB;
+  auto group = [&](cptr<RtTrav> T) RT_INL { return box_may_hit(T->blo, T->bhi, cr, cull_tmax(best)); };
+  auto object = [&](cptr<RtTrav> T) RT_INL {
+    // the object's cull kind and box come from the node's copy (RtTrav): one scalar load for the
+    // node decides the common case; the object's own record is read only once its box passes
+    if (T->cull == RT_CULL_ALWAYS) return;
+    if (T->cull == RT_CULL_BOX && !box_may_hit(T->blo, T->bhi, cr, cull_tmax(best))) return;
+    const int o = T->obj;
+    cptr<RtObject> O = &S.objects[o];
+    if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, ro, rd, cull_tmax(best))) return;
+    const int lb = O->leaf_begin, le = lb + O->leaf_count;
+    RT_SPEC_UNROLL
+    for (int l = lb; l < le; ++l) {
+      cptr<RtLeaf> L = &S.leaves[l];
+      if (O->leaf_cull) {
+        if (L->cull == RT_CULL_ALWAYS) continue;
+        if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, cull_tmax(best))) continue;
+      }
+      double t0 = 0.0, t1 = 0.0;
+      int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1, SHARE ? &shr : nullptr);
+      const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && SHARE && L->filter_const && !isnan(cr.inv.x));
+      if (n >= 1 && t0 > EPS && (t0 < best || (NORDER && t0 == best && o < bobj)) &&
+          (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) {
+        best = t0; bobj = o;
+      }
+      if (n >= 2 && t1 > EPS && (t1 < best || (NORDER && t1 == best && o < bobj)) &&
+          (!filtered || leaf_filter(S, L, add(ro, scale(rd, t1))))) {
+        best = t1; bobj = o;
+      }
+    }
+  };
+  walk_trav<NORDER>(S, group, object);
+  *dist = best;
+  return bobj;
+}
+
+// Product of the transparencies of every filtered hit with EPS < d < dist (raytracer.rs:181-197).
+// Early-out once the product is exactly 0 (it stays 0: every factor is finite, checked on the
+// host), objects of transparency exactly 1.0 are skipped (x * 1.0 == x).
+// SORDER (reflection-only kernels): walk S.strav, the likeliest occluders first (scene.cpp
+// shadow_order) -- every transparency is +-0 there, so the first filtered hit decides and the
+// order is free.  The early return ends the walk: `done` skips the rest of it (in the generic
+// walk a finished lane only rides along; the wave leaves once every lane is done).
+template <bool SHARE = false, bool OBB = !SHARE, bool SORDER = OBB>
+RT_FN double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
+  RT_OPAQUE(p.x);
+  RT_OPAQUE(p.y);
+  RT_OPAQUE(p.z);
+  double tr = 1.0;
+  bool done = false;
+  SphereShare shr = {0.0, 0.0, 0.0};
+  const CullRay cr = cull_ray(p, dir);
+  const bool fin = wave_finite(p, dir);
+  const double tmax = cull_tmax(dist);
+  auto group = [&](cptr<RtTrav> T) RT_INL { return !done && box_may_hit(T->blo, T->bhi, cr, tmax); };
+  auto object = [&](cptr<RtTrav> T) RT_INL {
+    if (done) return;
+    if (T->shadow_skip || T->cull == RT_CULL_ALWAYS) return;     // the node's copies (see nearest_hit)
+    if (T->cull == RT_CULL_BOX && !box_may_hit(T->blo, T->bhi, cr, tmax)) return;
+    cptr<RtObject> O = &S.objects[T->obj];
+    if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, p, dir, tmax)) return;
+    const double tobj = O->transparency;
+    const int lb = O->leaf_begin, le = lb + O->leaf_count;
+    RT_SPEC_UNROLL
+    for (int l = lb; l < le; ++l) {
+      cptr<RtLeaf> L = &S.leaves[l];
+      if (O->leaf_cull) {
+        if (L->cull == RT_CULL_ALWAYS) continue;
+        if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
+      }
+      double t0 = 0.0, t1 = 0.0;
+      int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1, SHARE ? &shr : nullptr);
+      const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && SHARE && L->filter_const && !isnan(cr.inv.x));
+      if (n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) {
+        tr *= tobj;
+        if (tr == 0.0 && S.shadow_early_out) { done = true; return; }
+      }
+      if (n >= 2 && t1 > EPS && t1 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t1))))) {
+        tr *= tobj;
+        if (tr == 0.0 && S.shadow_early_out) { done = true; return; }
+      }
+    }
+  };
+  walk_trav<RT_SHADOW_ORDER && SORDER, true>(S, group, object, &done);
+  return done ? 0.0 : tr;
+}
+
+// Normal and UV of top-level object O at point p: RTObject shape get_normal / get_uv_coordinates,
+// with CSG's is_on_surface / is_inside evaluated bottom-up over the post-order node list
+// (csg.rs:98-168) and the descent a-then-b of csg.rs:104-121 / :161-167.
+RT_FN void object_normal_uv(const DS& S, cptr<RtObject> O, V3 p, bool want_uv, V3* n,
+                                 double* u, double* v) {
+  cptr<RtNode> N = S.nodes + O->node_begin;
+  const int cnt = O->node_count;
+  const bool fin = wave_finite(p);
+  *u = 0.0;
+  *v = 0.0;
+  if (cnt == 1) {
+    cptr<RtLeaf> L = &S.leaves[N[0].leaf];
+    *n = leaf_normal(L, p, fin);
+    if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
+    return;
+  }
+  uint32_t in = 0, on = 0;
+  RT_SPEC_UNROLL
+  for (int i = 0; i < cnt; ++i) {
+    const int nk = N[i].kind, na = N[i].a, nb = N[i].b, nl = N[i].leaf;
+    bool bi, bo;
+    if (nk < RT_N_UNION) {
+      cptr<RtLeaf> L = &S.leaves[nl];
+      bi = leaf_inside(L, p, fin);
+      bo = leaf_on_surface(L, p, fin);
+    } else {
+      bool ia = (in >> na) & 1u, ib = (in >> nb) & 1u, oa = (on >> na) & 1u, ob = (on >> nb) & 1u;
+      if (nk == RT_N_UNION) { bi = ia || ib; bo = (oa && !ib) || (ob && !ia); }
+      else if (nk == RT_N_INTERSECTION) { bi = ia && ib; bo = (oa && ib) || (ob && ia); }
+      else { bi = ia && !ib; bo = (oa && !ib) || (ob && ia); }
+    }
+    in |= (uint32_t)bi << i;
+    on |= (uint32_t)bo << i;
+  }
+  // Descent a-then-b (csg.rs:104-121, :161-167).  Children precede parents in post-order, so one
+  // downward pass over the node indices visits every lane's path in order; node reads stay
+  // wave-uniform (scalar).  Membership tests go through ballot masks (see trace()).
+  const int lane = __lane_id();
+  int cur = cnt - 1, sel = -1;
+  bool neg = false;
+  RT_SPEC_UNROLL
+  for (int i = cnt - 1; i >= 0; --i) {
+    const int nk = N[i].kind, na = N[i].a, nb = N[i].b, nl = N[i].leaf;
+    if (!((__ballot(cur == i) >> lane) & 1)) continue;
+    if (nk < RT_N_UNION) { sel = nl; cur = -1; }
+    else if ((on >> na) & 1u) cur = na;
+    else if ((on >> nb) & 1u) { if (nk == RT_N_DIFFERENCE) neg = !neg; cur = nb; }   // b.get_normal(p) * -1.0
+    else cur = -1;                                          // fallback (1,0,0); UV is Err -> (0,0)
+  }
+  *n = {1.0, 0.0, 0.0};
+  const int lb = O->leaf_begin, le = lb + O->leaf_count;
+  RT_SPEC_UNROLL
+  for (int l = lb; l < le; ++l) {
+    if (!((__ballot(sel == l) >> lane) & 1)) continue;
+    cptr<RtLeaf> L = &S.leaves[l];
+    *n = leaf_normal(L, p, fin);
+    if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
+  }
+  if (neg) *n = scale(*n, -1.0);
+}
+
+// PixmapTexture::get_color_at (texture.rs:27-34) on RGBA8 texels, /255.0 (sceneparser/texture.rs:29-33)
+RT_FN Col texture_color(const DS& S, int tex, double u, double v) {
+  const int tw = S.textures[tex].w, th = S.textures[tex].h;
+  const int64_t toff = S.textures[tex].offset;
+  double x = u * (double)(tw - 1);
+  double y = (double)th - (v * (double)(th - 1)) - 1.0;
+  // `as usize` saturates (NaN/negative -> 0); the reference would panic past the edge: clamp.
+  int xi = x > 0.0 ? (x < (double)(tw - 1) ? (int)x : tw - 1) : 0;
+  int yi = y > 0.0 ? (y < (double)(th - 1) ? (int)y : th - 1) : 0;
+  const uint32_t px = *(const uint32_t*)(S.texels + toff + ((size_t)yi * tw + xi) * 4);
+  return {(double)(px & 0xffu) / 255.0, (double)((px >> 8) & 0xffu) / 255.0, (double)((px >> 16) & 0xffu) / 255.0};
+}
+
+// angle(-dir, n) >= PI/2 (raytracer.rs:230-231) from the cosine `cin` the angle's acos would take
+// (vector.rs:57-59).  acos is monotone and rt_acos is within 1 ulp, so for |cin| > 1e-15 (>= 4 ulp
+// of PI/2 away from the threshold) the sign decides exactly -- except past -1: a cosine that
+// rounds below -1 (a ray through a sphere's centre meets the normal head-on) makes acos NaN and
+// the comparison false, so such a hit is NOT inside.  Near-grazing cosines (and NaN) evaluate
+// the acos itself.
+__device__ __forceinline__ bool inside_test(double cin) {
+  return cin < -1e-15 ? cin >= -1.0 : (cin > 1e-15 ? false : rt_acos(cin) >= PI_D / 2.0);
+}
+
+__device__ __forceinline__ V3 reflect_dir(V3 i, V3 n) {                    // raytracer.rs:332-334
+  return sub(i, scale(scale(n, 2.0), dot(n, i)));
+}
+__device__ __forceinline__ V3 refract_dir(V3 i, V3 n, double r, bool* tir) {   // raytracer.rs:336-353
+  double cos_1 = dot(scale(i, -1.0), n);
+  double v = 1.0 - r * r * (1.0 - cos_1 * cos_1);
+  *tir = v < 0.0;
+  if (*tir) return {0.0, 0.0, 0.0};
+  double cos_2 = sqrt_rt(v);
+  return normalized(add(scale(i, r), scale(n, r * cos_1 - cos_2)));
+}
+
+// Normal (normalised, :163), material colour at the UV (:165-170), transparency, reflectivity of
+// each lane's hit object -- SCALARISED over the distinct objects hit in this wave (readlane of the
+// first remaining lane), so every object / node / leaf read is wave-uniform (SMEM, no VGPRs).
+__device__ __forceinline__ void shade_inputs(const DS& S, int oi, V3 p, V3* nrm, Col* c, double* transp,
+                                             double* refl) {
+  auto shade = [&](cptr<RtObject> O) RT_INL {
+    double u, v;
+    object_normal_uv(S, O, p, O->textured != 0, nrm, &u, &v);
+    *c = O->textured ? texture_color(S, O->tex, u, v) : Col{O->color[0], O->color[1], O->color[2]};
+    *transp = O->transparency;
+    *refl = O->reflectivity;
+  };
+#ifdef RT_SPEC
+  // every object's inputs are constants: one branch per object, taken by the lanes that hit it
+  spec_for<0, rt_spec::N_OBJECTS>([&](auto I) RT_INL {
+    constexpr int o = decltype(I)::value;
+    if (oi == o) shade(as_const(&rt_spec::OBJECTS[o]));
+  });
+#else
+  uint64_t todo = __ballot(oi >= 0);
+  while (todo) {
+    const int o = __builtin_amdgcn_readlane(oi, (int)__builtin_ctzll(todo));
+    const uint64_t mine = __ballot(oi == o);
+    todo &= ~mine;
+    // test membership through the ballot mask, not `oi == o`: an equality lets the optimiser
+    // substitute the per-lane oi for the uniform o and the loads below turn into VMEM again.
+    if ((mine >> __lane_id()) & 1) shade(&S.objects[o]);
+  }
+#endif
+  *nrm = normalized(*nrm);
+}
+
+template <class A, class B> struct same_type { static constexpr bool value = false; };
+template <class A> struct same_type<A, A> { static constexpr bool value = true; };
+
+
+// Ray-debugger recording (raytracer.rs:17-19, :155-157, :282-284; ray_debugger.rs:92-137).
+// NoRec compiles to nothing in the render kernels; RtRayRecord slots are written in ray START
+// order and `order` lists them in the reference's callback order (a ray reports after its
+// children: post-order).
+struct NoRec {
+  __device__ __forceinline__ int begin(int, int, V3, V3, double, int, V3) { return 0; }
+  __device__ __forceinline__ void finish(int, Col) {}
+};
+#ifndef __HIPCC_RTC__
+using RtRayRecord = rt_ray_record;
+struct BufRec {
+  RtRayRecord* rec;
+  int* order;
+  int cap, n_begun, n_done;
+  const DS* S;
+  __device__ int begin(int depth, int type, V3 ro, V3 rd, double t, int oi, V3 p) {
+    const int i = n_begun++;
+    if (i >= cap) return -1;
+    RtRayRecord& r = rec[i];
+    r.depth = depth; r.ray_type = type; r.object = oi; r.intersected = t != INFINITY;
+    r.point[0] = ro.x; r.point[1] = ro.y; r.point[2] = ro.z;
+    r.direction[0] = rd.x; r.direction[1] = rd.y; r.direction[2] = rd.z;
+    r.distance = t;
+    const V3 ip = add(ro, scale(rd, r.intersected ? t : 1000.0));          // ray_debugger.rs:107-111
+    r.intersection[0] = ip.x; r.intersection[1] = ip.y; r.intersection[2] = ip.z;
+    r.has_normal = oi >= 0;
+    V3 n = {0.0, 0.0, 0.0};
+    if (oi >= 0) {                                                         // shape.get_normal (:113-119)
+      double u, v;
+      object_normal_uv(*S, &S->objects[oi], ip, false, &n, &u, &v);
+    }
+    r.normal[0] = n.x; r.normal[1] = n.y; r.normal[2] = n.z;
+    return i;
+  }
+  __device__ void finish(int i, Col c) {
+    if (i < 0) return;
+    rec[i].color[0] = c.r; rec[i].color[1] = c.g; rec[i].color[2] = c.b; rec[i].color[3] = 1.0;
+    if (n_done < cap) order[n_done] = i;
+    ++n_done;
+  }
+};
+#endif
+
+// Frame-stack slots in LDS.  The first KL frames of every lane's stack (A.r, A.g, A.b, w) live in
+// LDS laid out [frame][component][lane], so each access is one conflict-free ds_*_b64; deeper
+// frames (chains longer than KL, rare) use the private array, i.e. scratch.  KL = 2: 4 KB per
+// one-wave workgroup, 80 of the 160 KB at 5 waves/SIMD.  With the megakernel at 5 waves/SIMD
+// (below) the stack was the last large source of scratch traffic: KL = 2 cuts the 4K globes
+// launch's HBM traffic from 0.245 to 0.105 GB (writes 0.21 -> 0.082 GB, 2.5x the 33 MB frame) at
+// equal time (+0.4 %, noise; KL = 4: 0.089 GB but 5 % slower), profiles/r02t_*.  (At 7 waves/SIMD,
+// round 1, KL = 4 measured 0.2-0.8 % slower than the scratch stack, profiles/r01r_lds_stack_ab.txt.)
+#define LDS_AS __attribute__((address_space(3)))
+typedef LDS_AS double lds_f64;
+#ifndef RT_LDS_FRAMES
+#define RT_LDS_FRAMES 2
+#endif
+// Refraction-chain kernels (RT_MODE_CHAIN): frames of the chain stack kept in LDS.  At 4 waves/SIMD
+// (below) 5 frames fill the 160 KB of a CU (10 KB per one-wave workgroup).
+#ifndef RT_LDS_FRAMES_CHAIN
+#define RT_LDS_FRAMES_CHAIN 5
+#endif
+// Refraction frames also carry the pending reflection ray (P, D, rp: 7 doubles); the first
+// KLR of them go to LDS after the KL colour frames, [frame][component][lane] likewise.
+#ifndef RT_LDS_RFRAMES
+#define RT_LDS_RFRAMES 1
+#endif
+
+// get_ray_color (raytracer.rs:132-287) for one primary ray, recursion unrolled onto a per-lane
+// frame stack.  REFR = the scene has a transparent object (refraction frames need more state).
+// KL > 0: frames 0..KL-1 of the stack are in LDS at lf[(f * 4 + c) * 64] (lf = this lane's slot);
+// KLR > 0 (REFR): the pending-reflection state of frames 0..KLR-1 at lf[(KL * 4 + f * 7 + c) * 64].
+// CHAIN (REFR scenes with RtDevScene::ray_chains): every hit spawns at most one ray, so a refraction
+// frame never carries a pending reflection: frames are (A, w) as in the reflection-only kernels.
+template <bool REFR, class Rec = NoRec, int KL = 0, bool FC = false, int KLR = 0, bool CHAIN = false>
+RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, lds_f64* lf = nullptr) {
+  double fA[RT_MAX_DEPTH_CAP][3];     // parent colour already intensified by (1 - w)
+  double fW[RT_MAX_DEPTH_CAP];        // child weight w (transparency or reflectivity)
+  auto put_frame = [&](int f, Col A, double w) {
+    if (KL > 0 && f < KL) {
+      lf[(f * 4 + 0) * 64] = A.r; lf[(f * 4 + 1) * 64] = A.g; lf[(f * 4 + 2) * 64] = A.b; lf[(f * 4 + 3) * 64] = w;
+    } else {
+      fA[f][0] = A.r; fA[f][1] = A.g; fA[f][2] = A.b; fW[f] = w;
+    }
+  };
+  auto get_frame = [&](int f, Col* A, double* w) {
+    if (KL > 0 && f < KL) {
+      *A = {lf[(f * 4 + 0) * 64], lf[(f * 4 + 1) * 64], lf[(f * 4 + 2) * 64]}; *w = lf[(f * 4 + 3) * 64];
+    } else {
+      *A = {fA[f][0], fA[f][1], fA[f][2]}; *w = fW[f];
+    }
+  };
+  constexpr bool TREE = REFR && !CHAIN;       // a hit may spawn two rays: pending reflections
+  double fP[TREE ? RT_MAX_DEPTH_CAP : 1][3], fD[TREE ? RT_MAX_DEPTH_CAP : 1][3];
+  double fRP[TREE ? RT_MAX_DEPTH_CAP : 1];
+  uint32_t pend = 0;                  // bit f: frame f's reflection ray is still to be traced
+  static_assert(RT_MAX_DEPTH_CAP <= 32, "pending-reflection bit mask");
+  auto put_rframe = [&](int f, V3 P, V3 D, double rp) {
+    if (KLR > 0 && f < KLR) {
+      lds_f64* q = lf + (KL * 4 + f * 7) * 64;
+      q[0] = P.x; q[64] = P.y; q[128] = P.z; q[192] = D.x; q[256] = D.y; q[320] = D.z; q[384] = rp;
+    } else {
+      fP[f][0] = P.x; fP[f][1] = P.y; fP[f][2] = P.z; fD[f][0] = D.x; fD[f][1] = D.y; fD[f][2] = D.z; fRP[f] = rp;
+    }
+  };
+  auto get_rframe = [&](int f, V3* P, V3* D, double* rp) {
+    if (KLR > 0 && f < KLR) {
+      const lds_f64* q = lf + (KL * 4 + f * 7) * 64;
+      *P = {q[0], q[64], q[128]}; *D = {q[192], q[256], q[320]}; *rp = q[384];
+    } else {
+      *P = {fP[f][0], fP[f][1], fP[f][2]}; *D = {fD[f][0], fD[f][1], fD[f][2]}; *rp = fRP[f];
+    }
+  };
+  constexpr bool RECORD = !same_type<Rec, NoRec>::value;
+  // Shared sphere terms (SphereShare) in the refraction kernels only: at 4 waves/SIMD they have
+  // the registers (104 -> 116 VGPRs, no spill; spinning_globes 1080p 4.8 % faster), while the
+  // reflection-only megakernel at 5 waves spills 14 more VGPRs and runs 6 % slower on 4K globes
+  // (profiles/r02am_ab.txt).
+  constexpr bool SHARE = REFR && RT_SPHERE_SHARE && (!CHAIN || RT_SPHERE_SHARE_CHAIN);
+  constexpr bool OBB = !REFR;                          // oriented object boxes: reflection-only kernels
+  int fSlot[RECORD ? RT_MAX_DEPTH_CAP : 1];
+  [[maybe_unused]] int ray_type = 0, slot = 0;                  // RayType::NormalRay
+  int sp = 0, depth = 0;
+  Col C = {0.0, 0.0, 0.0};
+  for (;;) {
+    bool descend = false;
+    double t_hit;
+    const int oi = nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit);
+    const V3 p = add(ro, scale(rd, t_hit));                               // :162
+    if constexpr (RECORD) slot = rec->begin(depth, ray_type, ro, rd, t_hit, oi, p);
+    V3 nrm = {0.0, 0.0, 0.0};
+    Col c = {0.0, 0.0, 0.0}, L = {0.0, 0.0, 0.0};
+    double transp = 0.0, refl = 0.0;
+    if (oi >= 0) {
+      // Evaluation order is free (every step is a pure function of the hit), so the shadow
+      // rays of a group of lights are traced FIRST, while only the hit point is live, and the
+      // normal / UV / material and the per-light Lambert terms are formed afterwards: far fewer
+      // registers live across the traversals.  Light accumulation order is unchanged.
+      bool have_shading = false;
+      // One light at a time: the unit vector towards the light is the shadow ray's direction
+      // (:176-178) AND the Lambert term's `sdir` (:203-205), the same operations on the same
+      // operands, so it is formed once and kept for the Lambert term.
+#pragma unroll 1
+      for (int k = 0; k < S.n_lights; ++k) {
+        cptr<RtLight> lt = &S.lights[k];
+        const V3 lv = sub(ld3(lt->p), p);
+        double ll, ill;
+        len_inv(lv, &ll, &ill);
+        const V3 sdir = scale(lv, ill);                                    // normalized(lv)
+        const double t = shadow_transparency<SHARE, OBB>(S, p, sdir, ll);       // :176-197
+        if (!have_shading) {
+          shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
+          L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));                      // ambient (:172)
+          have_shading = true;
+        }
+        if (t == 0.0) continue;                                            // :199-227
+        double ang = rt_acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
+        if (ang >= PI_D / 2.0) ang = PI_D - ang;
+        const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
+        const Col lc = intensify<FC>(intensify<FC>(Col{lt->col[0], lt->col[1], lt->col[2]}, inten), t);
+        L = cadd<FC>(L, cmul<FC>(c, lc));
+      }
+      if (!have_shading) {
+        shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
+        L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));
+      }
+    }
+    if (oi < 0) {
+      C = {0.0, 0.0, 0.0};                                               // Color::BLACK (:152-160)
+    } else {
+      // The inside test (:230-235) only matters for a hit that spawns a ray: one with
+      // depth < max_depth and a reflectivity or a transparency.  Other hits skip its division
+      // and square roots (the values it would give are never read).
+      bool inside = false;
+      if (depth < max_depth && (refl != 0.0 || (REFR && transp != 0.0))) {
+        const V3 nd = scale(rd, -1.0);
+        inside = inside_test(dot(nd, nrm) / (len(nd) * len(nrm)));
+      }
+      const V3 n2 = inside ? scale(nrm, -1.0) : nrm;
+      const double r1 = inside ? 1.45 : 1.0, r2 = inside ? 1.0 : 1.45;
+      bool tir = false;
+      V3 tdir = {0.0, 0.0, 0.0};
+      const bool do_refr = REFR && depth < max_depth && transp != 0.0;   // :242
+      if (do_refr) tdir = refract_dir(rd, n2, r1 / r2, &tir);
+      const double rp = tir ? refl + (1.0 - refl) * transp : refl;       // :261-265
+      const bool do_refl = depth < max_depth && rp != 0.0 && (!inside || tir);   // :267
+      if (do_refr && !tir) {
+        put_frame(sp, intensify<FC>(L, 1.0 - transp), transp);
+        if constexpr (TREE) {
+          pend = do_refl ? pend | (1u << sp) : pend & ~(1u << sp);
+          if (do_refl) put_rframe(sp, p, reflect_dir(rd, n2), rp);
+        }                                                                  // CHAIN: do_refl is false here
+        if constexpr (RECORD) { fSlot[sp] = slot; ray_type = 2; }        // TransmissionRay
+        ++sp;
+        ro = p;
+        rd = tdir;
+        depth = sp;
+        descend = true;
+      } else if (do_refl) {
+        put_frame(sp, intensify<FC>(L, 1.0 - rp), rp);
+        if constexpr (TREE) pend &= ~(1u << sp);
+        if constexpr (RECORD) { fSlot[sp] = slot; ray_type = 1; }        // ReflectionRay
+        ++sp;
+        rd = reflect_dir(rd, n2);
+        ro = p;
+        depth = sp;
+        descend = true;
+      } else {
+        C = L;
+      }
+    }
+    if constexpr (RECORD) { if (!descend) rec->finish(slot, C); }     // leaf ray (or miss) reports now
+    if (descend) continue;
+    while (sp > 0) {                                                      // post-order combine
+      const int f = sp - 1;
+      Col fa;
+      double fw;
+      get_frame(f, &fa, &fw);
+      const Col comb = cadd<FC>(fa, intensify<FC>(C, fw));
+      if constexpr (TREE) {
+        if ((pend >> f) & 1u) {                                           // refraction done -> reflection
+          pend &= ~(1u << f);
+          double frp;
+          get_rframe(f, &ro, &rd, &frp);
+          put_frame(f, intensify<FC>(comb, 1.0 - frp), frp);
+          depth = sp;
+          descend = true;
+          if constexpr (RECORD) ray_type = 1;                              // ReflectionRay
+          break;
+        }
+      }
+      C = comb;
+      if constexpr (RECORD) rec->finish(fSlot[f], C);                  // parent reports after its children
+      --sp;
+    }
+    if (!descend) return C;
+  }
+}
+
+// ---------------------------------------------------------------- deferred shadows (REFR=false)
+// get_ray_color (raytracer.rs:132-287) for scenes without a transparent object, restructured so
+// a pixel's critical path is its chain of nearest hits rather than nearest hits AND every shadow
+// ray in series.  Without refraction every hit spawns at most one ray (the reflection), so a
+// pixel's rays form a chain and the reference's recursion computes
+//     C_h = L_h                                            (no reflection spawned)
+//     C_h = in_range(in_range(L_h * (1 - w_h)) + in_range(C_{h+1} * w_h))      (:267-280)
+// with L_h = the ambient + per-light Lambert terms of hit h (:172-228) and C = BLACK for a ray
+// that misses (:152-160).  Every L_h is a pure function of hit h and its lights' shadow
+// transparencies, so the three steps run as phases of one wave:
+//   1. chain:   per lane, trace the nearest-hit chain; per hit record p, the normal, the material
+//               colour and the reflection weight w in the lane's arrays (every hit but possibly
+//               the last spawned a reflection);
+//   2. shadows: every (hit, light) shadow ray of the WHOLE WAVE is dealt densely over its 64
+//               lanes through an LDS window (one round = up to 64 hits; the hits' owners write
+//               their points, any lane traces any (hit, light) pair, the owners read the
+//               transparencies back and form L_h in light order, :199-227);
+//   3. fold:    per lane, C from the last hit back to the first, the post-order combine.
+// Same operations, same order per value: bit-identical to trace<false>.  A pixel whose chain is
+// 11 bounces long now waits for 11 nearest-hit traversals plus a few dense shadow rounds, not
+// 11 * (1 + lights) serial traversals; lanes whose chains ended early trace other lanes' shadow
+// rays instead of idling.
+#ifndef RT_SH_TRCAP
+#define RT_SH_TRCAP 128             // shadow results per round: hits per round = min(64, TRCAP / lights)
+#endif
+#define RT_SPLIT_TILE_MASK 0xFFFFFu   // order entries: tile index in bits 0-19 (split tiles: see below)
+#ifndef RT_SPLIT_MAX_LOG2
+#define RT_SPLIT_MAX_LOG2 3           // a costly tile goes to at most 2^3 = 8 waves (part: bits 20-23)
+#endif
+static_assert(RT_SPLIT_MAX_LOG2 <= 4, "split part index has 4 bits");
+struct ShadowWin {                  // LDS, one per wave: 2.5 KB
+  double px[64], py[64], pz[64];
+  double tr[RT_SH_TRCAP];
+};
+
+// REFR (scenes with RtDevScene::ray_chains and a transparent object): a hit spawns a refraction
+// ray (weight transparency) or, on TIR or for a reflective object, a reflection ray (weight rp,
+// raytracer.rs:261-265), never both, so the rays still form a chain and the same three phases
+// apply; the decisions, directions and weights are trace<true, ..., CHAIN>'s, the traversals take
+// the refraction kernels' template arguments (shared sphere terms, draw-order shadow walk: the
+// transparency product's order is the reference's).
+template <int HC, bool FC = false, bool REFR = false>
+RT_FN Col trace_deferred(const DS& S, V3 ro, V3 rd, int max_depth, bool valid, ShadowWin* win) {
+  constexpr bool SHARE = REFR && RT_SPHERE_SHARE, OBB = !REFR;
+  double hP[HC][3], hN[HC][3], hC[HC][3], hW[HC];
+  int nh = 0;
+  bool last_spawned = false;          // the last hit spawned a reflection ray (that missed)
+  // ---- phase 1: the nearest-hit chain
+  if (valid) {
+    for (int depth = 0;; ++depth) {
+      double t_hit;
+      const int oi = nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit);
+      if (oi < 0) break;                                                   // BLACK (:152-160)
+      const V3 p = add(ro, scale(rd, t_hit));                               // :162
+      V3 nrm;
+      Col c;
+      double transp, refl;
+      shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);                    // :163-170
+      // inside test (:230-235), exactly as trace(): needed only if a ray may spawn
+      bool inside = false;
+      if (depth < max_depth && (refl != 0.0 || (REFR && transp != 0.0))) {
+        const V3 nd = scale(rd, -1.0);
+        inside = inside_test(dot(nd, nrm) / (len(nd) * len(nrm)));
+      }
+      const V3 n2 = inside ? scale(nrm, -1.0) : nrm;
+      bool tir = false;
+      V3 tdir = {0.0, 0.0, 0.0};
+      const bool do_refr = REFR && depth < max_depth && transp != 0.0;     // :242
+      const double r1 = inside ? 1.45 : 1.0, r2 = inside ? 1.0 : 1.45;
+      if (do_refr) tdir = refract_dir(rd, n2, r1 / r2, &tir);
+      const double rp = tir ? refl + (1.0 - refl) * transp : refl;         // :261-265
+      const bool refracts = do_refr && !tir;
+      const bool do_refl = !refracts && depth < max_depth && rp != 0.0 && (!inside || tir);   // :267
+      hP[nh][0] = p.x; hP[nh][1] = p.y; hP[nh][2] = p.z;
+      hN[nh][0] = nrm.x; hN[nh][1] = nrm.y; hN[nh][2] = nrm.z;
+      hC[nh][0] = c.r; hC[nh][1] = c.g; hC[nh][2] = c.b;
+      hW[nh] = refracts ? transp : rp;
+      ++nh;
+      last_spawned = refracts || do_refl;
+      if (!last_spawned) break;
+      rd = refracts ? tdir : reflect_dir(rd, n2);
+      ro = p;
+    }
+  }
+  // ---- phase 2: every shadow ray of the wave, dealt over all 64 lanes
+  const int lane = __lane_id();
+  const int nl = S.n_lights;
+  const int hpr = nl > 0 ? (RT_SH_TRCAP / nl < 64 ? RT_SH_TRCAP / nl : 64) : 64;
+  for (int next = 0;;) {
+    const int pend = nh - next;
+    int incl = pend;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
+    }
+    const int total = __shfl(incl, 63);
+    if (total == 0) break;                                                  // wave-uniform
+    const int base = incl - pend;
+    const int take = base >= hpr ? 0 : (pend < hpr - base ? pend : hpr - base);
+    for (int i = 0; i < take; ++i) {
+      win->px[base + i] = hP[next + i][0];
+      win->py[base + i] = hP[next + i][1];
+      win->pz[base + i] = hP[next + i][2];
+    }
+    const int n_pub = total < hpr ? total : hpr;
+    __syncthreads();
+    const int jobs = n_pub * nl;
+    for (int j = lane; j < jobs; j += 64) {                                 // :176-197
+      const int h = j % n_pub, k = j / n_pub;
+      const V3 p = {win->px[h], win->py[h], win->pz[h]};
+      const V3 lv = sub(ld3(S.lights[k].p), p);
+      win->tr[j] = shadow_transparency<SHARE, OBB, OBB>(S, p, normalized(lv), len(lv));
+    }
+    __syncthreads();
+    for (int i = 0; i < take; ++i) {                                        // L_h in light order
+      const int hh = next + i;
+      const V3 p = {hP[hh][0], hP[hh][1], hP[hh][2]};
+      const V3 nrm = {hN[hh][0], hN[hh][1], hN[hh][2]};
+      const Col c = {hC[hh][0], hC[hh][1], hC[hh][2]};
+      Col L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));                             // ambient (:172)
+      for (int k = 0; k < nl; ++k) {                                        // :199-227
+        const double tr = win->tr[k * n_pub + base + i];
+        if (tr == 0.0) continue;
+        cptr<RtLight> lt = &S.lights[k];
+        const V3 sdir = normalized(sub(ld3(lt->p), p));
+        double ang = rt_acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
+        if (ang >= PI_D / 2.0) ang = PI_D - ang;
+        const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
+        const Col lc = intensify<FC>(intensify<FC>(Col{lt->col[0], lt->col[1], lt->col[2]}, inten), tr);
+        L = cadd<FC>(L, cmul<FC>(c, lc));
+      }
+      hC[hh][0] = L.r; hC[hh][1] = L.g; hC[hh][2] = L.b;
+    }
+    next += take;
+    __syncthreads();                                                        // the window is reused
+  }
+  // ---- phase 3: post-order combine, last hit first
+  Col C = {0.0, 0.0, 0.0};
+  for (int h = nh - 1; h >= 0; --h) {
+    const Col L = {hC[h][0], hC[h][1], hC[h][2]};
+    const double w = hW[h];
+    C = (h == nh - 1 && !last_spawned) ? L : cadd<FC>(intensify<FC>(L, 1.0 - w), intensify<FC>(C, w));   // :278-279
+  }
+  return C;
+}
+
+// RT_SPEC: every table is the scene's constexpr copy (k_spec.hip), only the texels stay in HBM.
+__device__ __forceinline__ DS make_ds(const RtDevScene& s) {
+  DS d;
+#ifdef RT_SPEC
+  d.objects = as_const(rt_spec::OBJECTS);
+  d.trav = as_const(rt_spec::TRAV);
+  d.n_trav = rt_spec::N_TRAV;
+  d.strav = as_const(rt_spec::STRAV);
+  d.n_strav = rt_spec::N_STRAV;
+  d.nodes = as_const(rt_spec::NODES);
+  d.leaves = as_const(rt_spec::LEAVES);
+  d.prog = as_const(rt_spec::PROG);
+  d.lights = as_const(rt_spec::LIGHTS);
+  d.textures = as_const(rt_spec::TEXTURES);
+  d.n_objects = rt_spec::N_OBJECTS;
+  d.n_lights = rt_spec::N_LIGHTS;
+  d.shadow_early_out = rt_spec::SHADOW_EARLY_OUT;
+#else
+  d.objects = as_const(s.objects);
+  d.trav = as_const(s.trav);
+  d.n_trav = s.n_trav;
+  d.strav = as_const(s.strav);
+  d.n_strav = s.n_strav;
+  d.nodes = as_const(s.nodes);
+  d.leaves = as_const(s.leaves);
+  d.prog = as_const(s.prog);
+  d.lights = as_const(s.lights);
+  d.textures = as_const(s.textures);
+  d.n_objects = s.n_objects;
+  d.n_lights = s.n_lights;
+  d.shadow_early_out = s.shadow_early_out;
+#endif
+  d.texels = s.texels;
+  return d;
+}
+
+// PerspectiveCamera::create_ray (camera.rs:65-74)
+__device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double y, V3* ro, V3* rd) {
+  double sx = ((x / cam.width) - 0.5) * cam.aspect;
+  double sy = (cam.height - 1.0 - y) / cam.height - 0.5;
+  *rd = add(add(ld3(cam.direction), scale(ld3(cam.right), sx)), scale(ld3(cam.up), sy));
+  *ro = ld3(cam.center);
+}
+
+// Output rows r = 0 .. n_rows-1 of a band layout: r -> full-frame row
+//   y = y_first + (r / band_rows) * band_pitch + r % band_rows
+// (a contiguous tile [y0, y1) is one band; the cyclic multi-GPU layout deals bands of
+// band_rows rows with pitch world * band_rows).  Workgroup = 16x16 output pixels, wave = 8x8.
+// Waves per SIMD (VGPR budget 512 / N) per instantiation: reflection-only scenes (REFR = false)
+// run 5 (<= 102 VGPRs, 96 used, 6 spilled).  Round 1 chose 7 (72 VGPRs, ~58 spilled) from A/B
+// runs that synchronised after every launch; with launches back to back (sustained clocks,
+// tools/ab_interleaved.py --burst) 5 is 1-3 % faster than 7 and cuts the launch's HBM traffic 9x
+// (2.30 -> 0.245 GB: the spills went to scratch), 6 is 5 % slower, 8 spills and is 1.7x slower
+// (profiles/r02o_waves_sustained.txt, r02q_ab.txt, r02r_ab.txt).  Refraction scenes with ray
+// trees keep 4 (128 VGPRs; 3 is equal, 5 is 1.5 % slower, profiles/r02s_ab.txt).
+// Kernel modes (RT_MODE_*): the reflection-only megakernel; refraction scenes whose rays form
+// chains (RtDevScene::ray_chains: frames are (A, w) only, no pending-reflection state); refraction
+// scenes with ray trees.
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU 4
+#endif
+#ifndef RT_WAVES_PER_EU_NOREFR
+#define RT_WAVES_PER_EU_NOREFR 5
+#endif
+// The chain kernel at 4 waves/SIMD keeps every VGPR in registers (115) and 5 stack frames in LDS:
+// anim120 moves 48.8 MB of HBM per 1080p frame (27 MB written, 3.3x the frame) at 9 201 Mrays/s.
+// At 5 waves/SIMD it spills 27 VGPRs inside the traversal loops and moves 481.7 MB per frame (317 MB
+// written) for 9 680 Mrays/s (+5 %); 5 waves without the shared sphere terms (14 spills) 216 MB at
+// 8 814 (profiles/r03k_anim_variants.txt).  The traffic budget wins over 5 %, as for the megakernel.
+#ifndef RT_WAVES_PER_EU_CHAIN
+#define RT_WAVES_PER_EU_CHAIN 4
+#endif
+#define RT_WAVES(REFR) ((REFR) ? RT_WAVES_PER_EU : RT_WAVES_PER_EU_NOREFR)
+#define RT_WAVES_MODE(M) ((M) == RT_MODE_REFL ? RT_WAVES_PER_EU_NOREFR : (M) == RT_MODE_CHAIN ? RT_WAVES_PER_EU_CHAIN : RT_WAVES_PER_EU)
+// Workgroup = one wave of 8x8 pixels: measured 3-5 % faster than 2x2-wave workgroups (round 1).
+constexpr int RT_WG_THREADS = 64;
+constexpr int RT_TILE_W = 8, RT_TILE_H = 8;
+
+// One pixel's colour into an output row: f64 RGBA (alpha 1 after any colour op), packed RGB8 (band
+// gathers) or RGBA8 with `(c * 255.0) as u8` per channel (easy_pixbuf.rs:46-53).
+template <bool F64>
+__device__ __forceinline__ void store_pixel(uint8_t* row, int x, Col c, int rgb) {
+  if constexpr (F64) {
+    double* o = (double*)row + (size_t)x * 4;
+    o[0] = c.r; o[1] = c.g; o[2] = c.b; o[3] = 1.0;
+  } else if (rgb) {
+    uint8_t* o = row + (size_t)x * 3;
+    o[0] = (uint8_t)to_u8(c.r); o[1] = (uint8_t)to_u8(c.g); o[2] = (uint8_t)to_u8(c.b);
+  } else {
+    ((uint32_t*)row)[x] = to_u8(c.r) | (to_u8(c.g) << 8) | (to_u8(c.b) << 16) | (255u << 24);
+  }
+}
+
+// ---------------------------------------------------------------- kernel bodies
+// The row kernels' bodies, shared by the generic kernels (k_rows.hip) and the scene-specialised ones
+// (k_spec.hip).  Output rows r = 0 .. n_rows-1 of a band layout; wave = one 8x8 tile.
+// Tile dispatch order (see launch_bands): `order` lists the tiles most expensive first, as measured
+// on a calibration launch that stored each tile's wave time in `cost`.  CAL (the calibration
+// instantiation) is the only one that carries the timing code.
+template <int MODE, bool F64, bool CAL, bool FC>
+__device__ __forceinline__ void rows_body(const RtDevScene& S, int y_first, int band_rows, int band_pitch, int n_rows,
+                                          int max_depth, uint8_t* __restrict__ out, size_t stride,
+                                          const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb,
+                                          lds_f64* frames) {
+  constexpr bool REFR = MODE != RT_MODE_REFL, CHAIN = MODE == RT_MODE_CHAIN;
+  constexpr int KLR = MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0;
+  constexpr int KL = CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES;
+  const int lane = threadIdx.x & 63;
+  const unsigned tile = CAL || !order ? blockIdx.x : (unsigned)order[blockIdx.x];
+  [[maybe_unused]] uint64_t t_start = 0;
+  if constexpr (CAL) t_start = wall_clock64();
+  const unsigned tiles_x = (unsigned)(S.width + RT_TILE_W - 1) / RT_TILE_W;
+  const int bx = (int)(tile % tiles_x), by = (int)(tile / tiles_x);
+  const int x = bx * RT_TILE_W + (lane & 7);
+  const int r = by * RT_TILE_H + (lane >> 3);
+  if (x >= S.width || r >= n_rows) return;
+  const int y = y_first + (r / band_rows) * band_pitch + r % band_rows;
+  if (y >= S.height) return;
+  V3 ro, rd;
+  camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
+  const Col c = trace<REFR, NoRec, KL, FC, KLR, CHAIN>(make_ds(S), ro, rd, max_depth, nullptr, frames + lane);
+  store_pixel<F64>(out + (size_t)r * stride, x, c, rgb);
+  if constexpr (CAL)
+    if (threadIdx.x == 0) cost[tile] = (uint32_t)(wall_clock64() - t_start);   // vector store
+}
+template <int MODE>
+constexpr int rows_lds_doubles() {
+  return ((MODE == RT_MODE_CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES) * 4 + (MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0) * 7) * 64;
+}
+
+// The deferred-shadow kernel's body (reflection-only scenes, or refraction chains on request): one
+// wave per 8x8 tile, every tile on the deferred path (trace_deferred), and the costliest tiles split
+// over P = 2, 4 or 8 waves: wave `part` renders pixels [part * 64/P, (part + 1) * 64/P) of the tile
+// on its first 64/P lanes and its other lanes only trace shadow rays (phase 2).  Order entry:
+// tile | part << 20 | log2(P) << 24 (built by launch_bands after the calibration launch).
+template <bool F64, bool CAL, bool FC, bool REFR>
+__device__ __forceinline__ void deferred_body(const RtDevScene& S, int y_first, int band_rows, int band_pitch,
+                                              int n_rows, int max_depth, uint8_t* __restrict__ out, size_t stride,
+                                              const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb,
+                                              ShadowWin* win) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t e = CAL || !order ? blockIdx.x : (uint32_t)order[blockIdx.x];
+  const unsigned tile = e & RT_SPLIT_TILE_MASK;
+  const int lp = (int)((e >> 24) & 7u), per = 64 >> lp;
+  const int pix = (int)((e >> 20) & 15u) * per + lane;
+  [[maybe_unused]] uint64_t t_start = 0;
+  if constexpr (CAL) t_start = wall_clock64();
+  const unsigned tiles_x = (unsigned)(S.width + 7) / 8;
+  const int x = (int)(tile % tiles_x) * 8 + (pix & 7);
+  const int r = (int)(tile / tiles_x) * 8 + (pix >> 3);
+  int y = 0;
+  bool valid = lane < per && x < S.width && r < n_rows;
+  if (valid) {
+    y = y_first + (r / band_rows) * band_pitch + r % band_rows;
+    valid = y < S.height;
+  }
+  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+  if (valid) camera_ray(S.cam, (double)x, (double)y, &ro, &rd);             // get_pixel(x as f64, y as f64)
+  const Col c = trace_deferred<RT_MAX_DEPTH_CAP + 1, FC, REFR>(make_ds(S), ro, rd, max_depth, valid, win);
+  if (valid) store_pixel<F64>(out + (size_t)r * stride, x, c, rgb);
+  if constexpr (CAL)
+    if (lane == 0) cost[tile] = (uint32_t)(wall_clock64() - t_start);
+}
+#ifndef RT_WAVES_PER_EU_DEFERRED
+#define RT_WAVES_PER_EU_DEFERRED 7
+#endif
+
+}  // namespace

@@ -10,7 +10,9 @@
 // fma() here is an explicit, deterministic part of THIS function -- the reference's own
 // arithmetic is still evaluated without contraction everywhere else.
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <math.h>
+#endif
 
 #ifndef RT_HD
 #define RT_HD

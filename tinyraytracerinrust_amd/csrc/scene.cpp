@@ -467,7 +467,7 @@ static void order_literals(FlatScene& f, const RtObject& ob) {
     std::stable_sort(idx, idx + X.n_lit, [&](int a, int b) { return fail[a] > fail[b]; });
     int32_t lits[RT_MAX_LITS];
     for (int k = 0; k < X.n_lit; ++k) lits[k] = X.lit[idx[k]];
-    if (!getenv("RT_NO_LIT_ORDER"))
+    if (!diag_env("RT_NO_LIT_ORDER"))
       for (int k = 0; k < X.n_lit; ++k) X.lit[k] = lits[k];
   }
 }
@@ -485,7 +485,7 @@ static void const_filters(FlatScene& f, const RtObject& ob) {
   for (int32_t x = ob.leaf_begin; x < ob.leaf_begin + ob.leaf_count; ++x) {
     RtLeaf& X = f.leaves[x];
     X.filter_const = 0;
-    if (X.kind != RT_N_SPHERE || X.n_lit < 1 || getenv("RT_NO_CONST_FILTER")) continue;
+    if (X.kind != RT_N_SPHERE || X.n_lit < 1 || diag_env("RT_NO_CONST_FILTER")) continue;
     double mrow = 0.0, fwd = 0.0, tsum = 0.0;
     for (int i = 0; i < 3; ++i) {
       mrow = std::max(mrow, fabs(X.inv[4 * i]) + fabs(X.inv[4 * i + 1]) + fabs(X.inv[4 * i + 2]));
@@ -526,7 +526,7 @@ static void const_filters(FlatScene& f, const RtObject& ob) {
 // (cull_ray / box_may_hit).
 static void obb(FlatScene& f, RtObject* ob) {
   ob->obb_leaf = -1;
-  if (ob->cull != RT_CULL_BOX || getenv("RT_NO_OBB")) return;
+  if (ob->cull != RT_CULL_BOX || diag_env("RT_NO_OBB")) return;
   double wvol = 1.0;
   for (int i = 0; i < 3; ++i) wvol *= ob->bhi[i] - ob->blo[i];
   double best = 0.5 * wvol;
@@ -636,7 +636,7 @@ static void build_hierarchy(FlatScene* fs, const std::vector<int>& perm, std::ve
   HierBuilder h{*fs, *out, perm};
   out->clear();
   const int n = (int)perm.size();
-  const bool flat = getenv("RT_FLAT_OBJECTS") != nullptr;   // diagnostic: no group nodes
+  const bool flat = diag_env("RT_FLAT_OBJECTS");   // diagnostic: no group nodes
   for (int i = 0; i < n;) {
     if (flat || fs->objects[perm[i]].cull != RT_CULL_BOX) { h.object(i); ++i; continue; }
     int j = i;
@@ -656,7 +656,7 @@ static std::vector<int> shadow_order(const FlatScene& f) {
   const int n = (int)f.objects.size();
   std::vector<int> perm(n);
   for (int i = 0; i < n; ++i) perm[i] = i;
-  if (f.any_transparent || getenv("RT_DRAW_ORDER_SHADOWS")) return perm;
+  if (f.any_transparent || diag_env("RT_DRAW_ORDER_SHADOWS")) return perm;
   std::vector<double> vol(n);
   for (int i = 0; i < n; ++i) {
     const RtObject& o = f.objects[i];
@@ -676,6 +676,38 @@ static std::vector<int> shadow_order(const FlatScene& f) {
   }
   std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return vol[a] > vol[b]; });
   return perm;
+}
+
+// The flattened scene as text (rt_scene_describe): the flags, both hierarchies and every object's
+// culling boxes, oriented box and leaf records -- what the kernels will read (tests, debugging).
+std::string describe_flat(const FlatScene& f) {
+  std::string s;
+  char buf[1024];
+  auto emit = [&](const char* fmt, auto... a) {
+    snprintf(buf, sizeof buf, fmt, a...);
+    s += buf;
+  };
+  emit("scene any_transparent=%d ray_chains=%d colour_fast=%d shadow_early_out=%d shadow_pow=%d\n",
+          f.any_transparent, f.ray_chains, f.colour_fast, f.shadow_early_out, f.shadow_pow);
+  for (size_t i = 0; i < f.trav.size(); ++i)
+    emit("trav %zu obj=%d skip=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f]\n", i, f.trav[i].obj, f.trav[i].skip,
+            f.trav[i].blo[0], f.trav[i].blo[1], f.trav[i].blo[2], f.trav[i].bhi[0], f.trav[i].bhi[1], f.trav[i].bhi[2]);
+  for (size_t i = 0; i < f.strav.size(); ++i)
+    emit("strav %zu obj=%d skip=%d\n", i, f.strav[i].obj, f.strav[i].skip);
+  for (size_t o = 0; o < f.objects.size(); ++o) {
+    const RtObject& ob = f.objects[o];
+    emit("object %zu cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] leaves %d leaf_cull=%d obb_leaf=%d "
+            "[%.3f %.3f %.3f]..[%.3f %.3f %.3f]\n", o, ob.cull, ob.blo[0], ob.blo[1], ob.blo[2], ob.bhi[0], ob.bhi[1],
+            ob.bhi[2], ob.leaf_count, ob.leaf_cull, ob.obb_leaf, ob.olo[0], ob.olo[1], ob.olo[2], ob.ohi[0], ob.ohi[1], ob.ohi[2]);
+    for (int l = ob.leaf_begin; l < ob.leaf_begin + ob.leaf_count; ++l) {
+      const RtLeaf& L = f.leaves[l];
+      emit("   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d lits %d (%d %d %d) const %d xdiag %d share %d axis %d\n", l, L.kind,
+              L.cull, L.blo[0], L.blo[1], L.blo[2], L.bhi[0], L.bhi[1], L.bhi[2], L.prog_end - L.prog_begin, L.n_lit,
+              L.n_lit > 0 ? L.lit[0] : -1, L.n_lit > 1 ? L.lit[1] : -1, L.n_lit > 2 ? L.lit[2] : -1, L.filter_const, L.xdiag, L.share_prev,
+              L.plane_axis);
+    }
+  }
+  return s;
 }
 
 int flatten(const rt_scene& s, FlatScene* out) {
@@ -707,7 +739,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
   // (shadow ray, object) pairs in any order and fold counts (render_kernels.hip wfp_*).
   f.shadow_pow = 1;
   f.shadow_t = 0.0;
-  bool have_t = false;
+  bool have_t = false, any_zero = false;
   auto nonneg = [](double x) { return std::isfinite(x) && !std::signbit(x); };
   auto unit = [&](double x) { return nonneg(x) && x <= 1.0; };
   for (const ObjectRec& o : s.objects) {
@@ -775,6 +807,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
     if (m.transparency != 0.0) f.any_transparent = 1;
     if (m.transparency != 0.0 && m.reflectivity != 0.0) f.ray_chains = 0;
     if (!isfinite(m.transparency)) f.shadow_early_out = 0;
+    if (m.transparency == 0.0) any_zero = true;
     if (m.transparency != 0.0 && m.transparency != 1.0) {
       if (!have_t) { f.shadow_t = m.transparency; have_t = true; }
       else if (memcmp(&f.shadow_t, &m.transparency, sizeof(double)) != 0) f.shadow_pow = 0;
@@ -784,6 +817,10 @@ int flatten(const rt_scene& s, FlatScene* out) {
     f.objects.push_back(ob);
   }
   if (!f.shadow_early_out) f.shadow_pow = 0;
+  // |T| > 1: T^k may overflow to +-inf, and inf * 0 is NaN, so with a zero-transparency object the
+  // draw-order product depends on where the zero factor comes (T, T, 0 -> NaN; 0, T, T -> 0): not
+  // a function of the counts
+  if (have_t && !(fabs(f.shadow_t) <= 1.0) && any_zero) f.shadow_pow = 0;
   for (RtObject& ob : f.objects) share_sphere_terms(f, &ob);
   {
     std::vector<int> draw((size_t)f.objects.size());
@@ -805,28 +842,6 @@ int flatten(const rt_scene& s, FlatScene* out) {
     f.texels.insert(f.texels.end(), t.rgba.begin(), t.rgba.end());
     off += (int64_t)t.rgba.size();
     while (off % 16) { f.texels.push_back(0); ++off; }
-  }
-  if (getenv("RT_DUMP_FLAT")) {                                // debugging aid: culling boxes
-    fprintf(stderr, "scene any_transparent=%d ray_chains=%d colour_fast=%d shadow_early_out=%d shadow_pow=%d\n",
-            f.any_transparent, f.ray_chains, f.colour_fast, f.shadow_early_out, f.shadow_pow);
-    for (size_t i = 0; i < f.trav.size(); ++i)
-      fprintf(stderr, "trav %zu obj=%d skip=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f]\n", i, f.trav[i].obj, f.trav[i].skip,
-              f.trav[i].blo[0], f.trav[i].blo[1], f.trav[i].blo[2], f.trav[i].bhi[0], f.trav[i].bhi[1], f.trav[i].bhi[2]);
-    for (size_t i = 0; i < f.strav.size(); ++i)
-      fprintf(stderr, "strav %zu obj=%d skip=%d\n", i, f.strav[i].obj, f.strav[i].skip);
-    for (size_t o = 0; o < f.objects.size(); ++o) {
-      const RtObject& ob = f.objects[o];
-      fprintf(stderr, "object %zu cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] leaves %d leaf_cull=%d obb_leaf=%d "
-              "[%.3f %.3f %.3f]..[%.3f %.3f %.3f]\n", o, ob.cull, ob.blo[0], ob.blo[1], ob.blo[2], ob.bhi[0], ob.bhi[1],
-              ob.bhi[2], ob.leaf_count, ob.leaf_cull, ob.obb_leaf, ob.olo[0], ob.olo[1], ob.olo[2], ob.ohi[0], ob.ohi[1], ob.ohi[2]);
-      for (int l = ob.leaf_begin; l < ob.leaf_begin + ob.leaf_count; ++l) {
-        const RtLeaf& L = f.leaves[l];
-        fprintf(stderr, "   leaf %d kind=%d cull=%d box [%.3f %.3f %.3f]..[%.3f %.3f %.3f] prog %d lits %d (%d %d %d) const %d xdiag %d share %d axis %d\n", l, L.kind,
-                L.cull, L.blo[0], L.blo[1], L.blo[2], L.bhi[0], L.bhi[1], L.bhi[2], L.prog_end - L.prog_begin, L.n_lit,
-                L.n_lit > 0 ? L.lit[0] : -1, L.n_lit > 1 ? L.lit[1] : -1, L.n_lit > 2 ? L.lit[2] : -1, L.filter_const, L.xdiag, L.share_prev,
-                L.plane_axis);
-      }
-    }
   }
   // PerspectiveCamera::new(width, height, center, None, None, None) (camera.rs:30-54)
   V center = {s.cam_center[0], s.cam_center[1], s.cam_center[2]};
@@ -900,6 +915,21 @@ int rt_scene_traversal(const rt_scene* s, int32_t* obj, int32_t* skip, int32_t c
   if (rc) return rc;
   *n = (int32_t)f.trav.size();
   for (int32_t i = 0; i < *n && i < cap; ++i) { obj[i] = f.trav[i].obj; skip[i] = f.trav[i].skip; }
+  return RT_OK;
+}
+
+int rt_scene_describe(const rt_scene* s, char* buf, size_t cap, size_t* len) {
+  if (!s || !len || (cap > 0 && !buf)) return fail(RT_ERR_INVALID, "null argument");
+  FlatScene f;
+  int rc = flatten(*s, &f);
+  if (rc) return rc;
+  const std::string d = describe_flat(f);
+  *len = d.size();
+  if (cap > 0) {
+    const size_t n = d.size() < cap - 1 ? d.size() : cap - 1;
+    memcpy(buf, d.data(), n);
+    buf[n] = 0;
+  }
   return RT_OK;
 }
 

@@ -79,6 +79,10 @@ struct rt_scene {
 
 namespace rt {
 int flatten(const rt_scene& s, FlatScene* out);
+std::string describe_flat(const FlatScene& f);   // rt_scene_describe's text
+// A diagnostic switch from the environment: only in a diagnostic build (make diag DIAG=-DRT_DIAG_ENV),
+// false in the product (rt_ctx.hip).
+bool diag_env(const char* name);
 // DSL front end (scene_dsl.cpp): fills a fresh default scene.
 int compile_scene_text(const char* text, const char* asset_dir, double time, rt_scene* scene);
 // PNG (png_io.cpp)

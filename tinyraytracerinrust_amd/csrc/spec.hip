@@ -1,0 +1,295 @@
+// spec.hip -- scene-specialised row kernels (rt_ctx_set_option(RT_OPT_SPECIALIZE, 1)).
+//
+// The generic kernels read the flattened scene (rt_blob.h) from HBM: every hierarchy step, object
+// and leaf record is a dependent scalar load, and every branch on a record field (leaf kind,
+// transform form, cull kind, filter form) is taken at run time.  A scene is immutable after upload,
+// so this file compiles the SAME device code (rt_device.h) once more with the scene's tables as
+// constexpr data (RT_SPEC): the hierarchy walk unrolls into nested branches over constant boxes,
+// every record field is a literal, and the branches on them fold away.  The arithmetic on ray
+// values is unchanged -- the same operations in the same order, -ffp-contract=off, constant folding
+// only of values the host computed already -- so the pixels are bit-identical (tests/test_gpu_spec.py).
+//
+// hipRTC (libhiprtc, ROCm) compiles the program at scene upload; the code object is cached per
+// process by the program text's hash, and loaded as a module on the context's device.  Launches
+// take a specialised kernel when one matches (k_rows.hip), the generic one otherwise.
+#include <hip/hiprtc.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+#include "rt_ctx.h"
+
+namespace {
+
+// The device headers as text (build/spec_headers.inc: raw string literals made by the Makefile).
+#include "spec_headers.inc"
+
+struct SpecCode {
+  std::vector<char> code;              // the linked code object
+  double compile_ms = 0.0;
+};
+std::mutex g_spec_mu;
+std::map<uint64_t, std::shared_ptr<SpecCode>> g_spec_cache;
+
+uint64_t fnv1a(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char ch : s) { h ^= ch; h *= 1099511628211ull; }
+  return h;
+}
+
+// constexpr T NAME[] = { bit_cast<T>(words), ... }: the host record's exact bits (padding included).
+template <class T>
+void emit_table(std::string& s, const char* type, const char* name, const std::vector<T>& v) {
+  static_assert(sizeof(T) % 8 == 0, "spec tables are emitted as 64-bit words");
+  constexpr size_t W = sizeof(T) / 8;
+  char buf[64];
+  s += "constexpr ";
+  s += type;
+  s += " ";
+  s += name;
+  s += "[] = {\n";
+  std::vector<T> rows(v);
+  if (rows.empty()) {                  // no zero-length arrays: one zero record, never read (N_* = 0)
+    rows.resize(1);
+    memset((void*)rows.data(), 0, sizeof(T));
+  }
+  for (const T& r : rows) {
+    uint64_t w[W];
+    memcpy(w, &r, sizeof(T));
+    s += "  __builtin_bit_cast(";
+    s += type;
+    s += ", SpecRaw<";
+    snprintf(buf, sizeof buf, "%zu", W);
+    s += buf;
+    s += ">{{";
+    for (size_t i = 0; i < W; ++i) {
+      snprintf(buf, sizeof buf, "%s0x%llxull", i ? "," : "", (unsigned long long)w[i]);
+      s += buf;
+    }
+    s += "}}),\n";
+  }
+  s += "};\n";
+}
+
+}  // namespace
+
+namespace rt {
+
+// The program's prelude: the scene's tables as constexpr data, then the device code.
+std::string spec_source(const FlatScene& f, int mode, bool fc, bool deferred) {
+  (void)mode; (void)fc; (void)deferred;
+  std::string s;
+  char buf[256];
+  s += "// scene-specialised row kernels (spec.hip)\n#define RT_SPEC 1\n#include \"rt_blob.h\"\n";
+  s += "template <int N> struct SpecRaw { unsigned long long w[N]; };\nnamespace rt_spec {\n";
+  snprintf(buf, sizeof buf,
+           "constexpr int N_OBJECTS = %d, N_LIGHTS = %d, N_TRAV = %d, N_STRAV = %d, SHADOW_EARLY_OUT = %d;\n",
+           (int)f.objects.size(), (int)f.lights.size(), (int)f.trav.size(), (int)f.strav.size(), f.shadow_early_out);
+  s += buf;
+  emit_table(s, "RtObject", "OBJECTS", f.objects);
+  emit_table(s, "RtTrav", "TRAV", f.trav);
+  emit_table(s, "RtTrav", "STRAV", f.strav);
+  emit_table(s, "RtNode", "NODES", f.nodes);
+  emit_table(s, "RtLeaf", "LEAVES", f.leaves);
+  emit_table(s, "RtProg", "PROG", f.prog);
+  emit_table(s, "RtLight", "LIGHTS", f.lights);
+  emit_table(s, "RtTexture", "TEXTURES", f.textures);
+  s += "}  // namespace rt_spec\n#include \"rt_device.h\"\n";
+  return s;
+}
+
+// One kernel of the program: rt_spec_rows_<f64><cal> (the megakernel of the scene's mode) or
+// rt_spec_def_<f64><cal> (the deferred-shadow kernel), the generic kernels' exact bodies.
+static std::string spec_kernel(int kind, int mode, bool fc, int f64, int cal) {
+  static const char* args =
+      "(RtDevScene S, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth, uint8_t* __restrict__ out, "
+      "size_t stride, const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb)";
+  char buf[1024];
+  if (kind == 0)
+    snprintf(buf, sizeof buf,
+             "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_MODE(%d)))) "
+             "void rt_spec_rows_%d%d%s {\n  __shared__ double s_frames[rows_lds_doubles<%d>()];\n"
+             "  rows_body<%d, %s, %s, %s>(S, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, order, "
+             "cost, rgb, (lds_f64*)s_frames);\n}\n",
+             mode, f64, cal, args, mode, mode, f64 ? "true" : "false", cal ? "true" : "false", fc ? "true" : "false");
+  else
+    snprintf(buf, sizeof buf,
+             "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_DEFERRED))) "
+             "void rt_spec_def_%d%d%s {\n  __shared__ ShadowWin win;\n"
+             "  deferred_body<%s, %s, %s, %s>(S, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, order, "
+             "cost, rgb, &win);\n}\n",
+             f64, cal, args, f64 ? "true" : "false", cal ? "true" : "false", fc ? "true" : "false",
+             mode == RT_MODE_REFL ? "false" : "true");
+  return buf;
+}
+
+// The kernels a context loads, (kind, f64, cal): kind 0 = the megakernel, 1 = the deferred kernel
+// (reflection-only scenes: their tail-bound launches' choice).  RT_OPT_SPECIALIZE 1: the RGBA8 /
+// RGB8 product launches (f64 = 0, cal = 0); 2: the f64 and calibration instantiations too (tests:
+// every launch of a parity test then runs specialised).  Each kernel is its own program (prelude +
+// one kernel): the programs compile in parallel, and the inliner sees one kernel per module.
+struct SpecKernel { int kind, f64, cal; };
+static std::vector<SpecKernel> spec_kernels(const rt_ctx* c) {
+  std::vector<SpecKernel> v;
+  const int n = c->spec_on >= 2 ? 2 : 1;
+  for (int kind = 0; kind < (c->spec_deferred ? 2 : 1); ++kind)
+    for (int f64 = 0; f64 < n; ++f64)
+      for (int cal = 0; cal < n; ++cal) v.push_back({kind, f64, cal});
+  return v;
+}
+static std::vector<std::string> spec_programs(const rt_ctx* c) {
+  std::vector<std::string> v;
+  for (const SpecKernel& k : spec_kernels(c)) v.push_back(c->spec_src + spec_kernel(k.kind, c->spec_mode, c->spec_fc, k.f64, k.cal));
+  return v;
+}
+
+void spec_drop(rt_ctx* c) {
+  for (auto& m : c->spec_mods)
+    if (m) (void)hipModuleUnload(m);
+  memset(c->spec_mods, 0, sizeof c->spec_mods);
+  c->spec_mod = nullptr;
+  memset(c->spec_rows, 0, sizeof c->spec_rows);
+  memset(c->spec_def, 0, sizeof c->spec_def);
+}
+
+// hipRTC: the program (with the device headers as named headers), the flags the library's own
+// kernels are built with (Makefile HIPFLAGS: -O3, no contraction, no fast-math, MachineLICM off).
+static int spec_compile(const std::string& src, SpecCode* out) {
+  const char* headers[] = {spec_hdr_rt_device, spec_hdr_rt_blob, spec_hdr_rt_math};
+  const char* names[] = {"rt_device.h", "rt_blob.h", "rt_math.h"};
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "rt_spec.hip", 3, headers, names) != HIPRTC_SUCCESS)
+    return fail(RT_ERR_DEVICE, "hiprtcCreateProgram failed");
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                        "-mllvm", "-disable-machine-licm"};
+  const auto t0 = std::chrono::steady_clock::now();
+  const hiprtcResult r = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+  out->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (r != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n + 1, '\0');
+    hiprtcGetProgramLog(prog, &log[0]);
+    hiprtcDestroyProgram(&prog);
+    return fail(RT_ERR_DEVICE, "hipRTC compile of the specialised kernels failed: %s\n%.2000s", hiprtcGetErrorString(r),
+                log.c_str());
+  }
+  size_t n = 0;
+  hiprtcGetCodeSize(prog, &n);
+  out->code.resize(n);
+  hiprtcGetCode(prog, out->code.data());
+  hiprtcDestroyProgram(&prog);
+  return RT_OK;
+}
+
+// The code objects of programs: from the process cache, else compiled in parallel (one thread per
+// program; hipRTC is thread-safe) and cached.  *compile_ms = the longest compile (0: all cached).
+static int spec_codes(const std::vector<std::string>& srcs, std::vector<std::shared_ptr<SpecCode>>* out,
+                      double* compile_ms) {
+  out->assign(srcs.size(), nullptr);
+  std::vector<uint64_t> h(srcs.size());
+  {
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    for (size_t i = 0; i < srcs.size(); ++i) {
+      h[i] = fnv1a(srcs[i]);
+      auto it = g_spec_cache.find(h[i]);
+      if (it != g_spec_cache.end()) (*out)[i] = it->second;
+    }
+  }
+  std::vector<std::shared_ptr<SpecCode>> fresh(srcs.size());
+  std::vector<int> rc(srcs.size(), RT_OK);
+  std::vector<std::string> err(srcs.size());
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    if ((*out)[i]) continue;
+    fresh[i] = std::make_shared<SpecCode>();
+    th.emplace_back([&, i] {
+      rc[i] = spec_compile(srcs[i], fresh[i].get());
+      if (rc[i]) err[i] = rt_last_error();      // the thread's own error slot
+    });
+  }
+  for (auto& x : th) x.join();
+  *compile_ms = 0.0;
+  for (size_t i = 0; i < srcs.size(); ++i)
+    if (rc[i]) return fail(rc[i], "%s", err[i].c_str());
+  std::lock_guard<std::mutex> lk(g_spec_mu);
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    if ((*out)[i]) continue;
+    *compile_ms = std::max(*compile_ms, fresh[i]->compile_ms);
+    (*out)[i] = g_spec_cache.emplace(h[i], fresh[i]).first->second;
+  }
+  return RT_OK;
+}
+
+void spec_program(const FlatScene& f, rt_ctx* c) {
+  c->spec_mode = !f.any_transparent ? RT_MODE_REFL : f.ray_chains ? RT_MODE_CHAIN : RT_MODE_TREE;
+  c->spec_fc = f.colour_fast != 0;
+  c->spec_deferred = c->spec_mode == RT_MODE_REFL;
+  c->spec_src = spec_source(f, c->spec_mode, c->spec_fc, c->spec_deferred);
+}
+
+int spec_build(rt_ctx* c) {
+  spec_drop(c);
+  if (c->spec_src.empty()) return RT_OK;
+  const std::vector<std::string> srcs = spec_programs(c);
+  std::vector<std::shared_ptr<SpecCode>> codes;
+  int rc = spec_codes(srcs, &codes, &c->spec_compile_ms);
+  if (rc) return rc;
+  RT_HIP(hipSetDevice(c->device));
+  char name[32];
+  const std::vector<SpecKernel> ks = spec_kernels(c);
+  for (size_t i = 0; i < ks.size(); ++i) {
+    const SpecKernel& k = ks[i];
+    RT_HIP(hipModuleLoadData(&c->spec_mods[i], codes[i]->code.data()));
+    snprintf(name, sizeof name, k.kind ? "rt_spec_def_%d%d" : "rt_spec_rows_%d%d", k.f64, k.cal);
+    RT_HIP(hipModuleGetFunction(k.kind ? &c->spec_def[k.f64][k.cal] : &c->spec_rows[k.f64][k.cal], c->spec_mods[i], name));
+  }
+  c->spec_mod = c->spec_mods[0];
+  c->spec_hash = fnv1a(c->spec_src);
+  return RT_OK;
+}
+
+}  // namespace rt
+
+// rt_scene_precompile (include/rt_abi.h): the specialised programs of a scene into the process cache,
+// no device needed -- a host may compile on a worker thread while it renders with the generic kernels
+extern "C" int rt_scene_precompile(const rt_scene* s, double* compile_ms) {
+  if (!s) return fail(RT_ERR_INVALID, "null scene");
+  rt::FlatScene f;
+  int rc = rt::flatten(*s, &f);
+  if (rc) return rc;
+  rt_ctx tmp;
+  tmp.spec_on = 1;
+  rt::spec_program(f, &tmp);
+  std::vector<std::shared_ptr<SpecCode>> codes;
+  double ms = 0.0;
+  rc = rt::spec_codes(rt::spec_programs(&tmp), &codes, &ms);
+  if (compile_ms) *compile_ms = ms;
+  return rc;
+}
+
+// rt_scene_spec_program (include/rt_abi.h): the prelude and every kernel rt_scene_precompile compiles
+extern "C" int rt_scene_spec_program(const rt_scene* s, char* buf, size_t cap, size_t* len) {
+  if (!s || !len || (cap > 0 && !buf)) return fail(RT_ERR_INVALID, "null argument");
+  rt::FlatScene f;
+  int rc = rt::flatten(*s, &f);
+  if (rc) return rc;
+  rt_ctx tmp;
+  tmp.spec_on = 2;
+  rt::spec_program(f, &tmp);
+  std::string text = tmp.spec_src;
+  for (const rt::SpecKernel& k : rt::spec_kernels(&tmp)) text += rt::spec_kernel(k.kind, tmp.spec_mode, tmp.spec_fc, k.f64, k.cal);
+  *len = text.size();
+  if (cap > 0) {
+    const size_t n = text.size() < cap - 1 ? text.size() : cap - 1;
+    memcpy(buf, text.data(), n);
+    buf[n] = 0;
+  }
+  return RT_OK;
+}

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys as _sys
 from typing import Iterable, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -157,6 +158,29 @@ class Scene:
         obj, skip = (ctypes.c_int32 * max(1, n.value))(), (ctypes.c_int32 * max(1, n.value))()
         check(lib().rt_scene_traversal(self.h, obj, skip, n.value, ctypes.byref(n)))
         return [(obj[i], skip[i]) for i in range(n.value)]
+
+    def describe(self) -> str:
+        """rt_scene_describe: the flattened scene (flags, hierarchies, culling records) as text."""
+        n = ctypes.c_size_t()
+        check(lib().rt_scene_describe(self.h, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        check(lib().rt_scene_describe(self.h, buf, n.value + 1, ctypes.byref(n)))
+        return buf.value.decode()
+
+    def spec_program(self) -> str:
+        """rt_scene_spec_program: the scene-specialised program's text (RT_OPT_SPECIALIZE)."""
+        n = ctypes.c_size_t()
+        check(lib().rt_scene_spec_program(self.h, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        check(lib().rt_scene_spec_program(self.h, buf, n.value + 1, ctypes.byref(n)))
+        return buf.value.decode()
+
+    def precompile(self) -> float:
+        """rt_scene_precompile: compile the specialised program into the process cache (no device);
+        returns the hipRTC milliseconds (0 when cached)."""
+        ms = ctypes.c_double()
+        check(lib().rt_scene_precompile(self.h, ctypes.byref(ms)))
+        return ms.value
 
     def camera(self) -> dict:
         out = (ctypes.c_double * 13)()
@@ -315,6 +339,22 @@ class Renderer:
         walks the hierarchy for 64 rays, 1 (default) levels >= 1 as (ray, object) pairs sorted by
         object, 2 every level (same pixels)."""
         check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_WAVEFRONT_PAIRS, int(mode)))
+
+    def set_specialize(self, level: int = 1) -> None:
+        """rt_ctx_set_option(RT_OPT_SPECIALIZE): 0 the precompiled kernels; 1 compile the uploaded scene's
+        RGBA8 / RGB8 row kernels with the scene as constants (hipRTC, seconds per new scene; same pixels);
+        2 its f64 and calibration kernels too."""
+        check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_SPECIALIZE, int(level)))
+
+    def kernel_info(self) -> str:
+        """rt_ctx_kernel_info: generic or scene-specialised kernels, and what the last row launch ran."""
+        buf = ctypes.create_string_buffer(512)
+        check(lib().rt_ctx_kernel_info(self.h, buf, 512))
+        return buf.value.decode()
+
+    def kernel_variant(self) -> str:
+        """"spec" when the context holds scene-specialised kernels, else "generic"."""
+        return "spec" if self.kernel_info().startswith("scene-specialised") else "generic"
 
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()
@@ -553,7 +593,16 @@ class HwStream:
     """A HIP stream on a hardware queue of its own (rt_stream_create), usable as a torch stream
     (``.torch``, a torch.cuda.ExternalStream).  Renders meant to overlap go on such streams: plain
     torch / HIP streams share the process's few hardware queues, and two renders on one queue run
-    one after the other (include/rt_abi.h rt_stream_create)."""
+    one after the other (include/rt_abi.h rt_stream_create).
+
+    Lifetime: close() (or ``with HwStream() as s``) synchronises and destroys the stream.  Streams
+    still open when the interpreter exits are closed by an atexit hook, while the HIP runtime is
+    still up: a stream left for the runtime's own teardown (__cxa_finalize) was destroyed after a
+    profiler's intercept tables were gone, and rocprofv3 runs died there with SIGSEGV
+    (gpurun_out/r03j_kt.err, round-3 VERDICT).  __del__ never destroys a stream during interpreter
+    finalisation."""
+
+    _live: "weakref.WeakSet[HwStream]"
 
     def __init__(self, device: int = 0):
         import torch
@@ -561,13 +610,37 @@ class HwStream:
         check(lib().rt_stream_create(device, ctypes.byref(h)))
         self.handle = h.value
         self.torch = torch.cuda.ExternalStream(self.handle, device=torch.device("cuda", device))
+        HwStream._register(self)
+
+    @classmethod
+    def _register(cls, s: "HwStream") -> None:
+        if not hasattr(cls, "_live"):
+            import atexit
+            import weakref
+            cls._live = weakref.WeakSet()
+            atexit.register(cls.close_all)
+        cls._live.add(s)
+
+    @classmethod
+    def close_all(cls) -> None:
+        for s in list(getattr(cls, "_live", ())):
+            s.close()
 
     def close(self) -> None:
         if getattr(self, "handle", None):
+            self.torch.synchronize()
             lib().rt_stream_destroy(ctypes.c_void_p(self.handle))
             self.handle = None
 
+    def __enter__(self) -> "HwStream":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
     def __del__(self):
+        if _sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:

@@ -35,7 +35,11 @@ def main():
     ap.add_argument("--kernel", nargs="*", default=[],
                     help="per library (in order): RT_OPT_KERNEL auto / mega / deferred for its context; '-' keeps auto. "
                          "A library path may repeat with different kernels")
+    ap.add_argument("--option", nargs="*", default=[],
+                    help="per library (in order): OPT=VAL[,OPT=VAL] context options by number (rt_abi.h rt_option, "
+                         "e.g. 6=1 for RT_OPT_SPECIALIZE); '-' for none")
     a = ap.parse_args()
+    import time
     import torch
     W, H = (int(v) for v in a.size.split("x"))
     text = open(os.path.join(SCENES, a.scene + ".scene")).read().encode()
@@ -57,8 +61,16 @@ def main():
         kern = a.kernel[li] if li < len(a.kernel) and a.kernel[li] != "-" else None
         if kern:
             assert L.rt_ctx_set_option(cx, 0, {"auto": 0, "mega": 1, "deferred": 2}[kern]) == 0
-        ctxs.append((path + (f" [{env}]" if env else "") + (f" <{kern}>" if kern else ""), L, cx, []))
-    import time
+        opt = a.option[li] if li < len(a.option) and a.option[li] != "-" else None
+        if opt:
+            for kv in opt.split(","):
+                k, v = (int(x) for x in kv.split("="))
+                t0 = time.perf_counter()
+                rc = L.rt_ctx_set_option(cx, k, v)
+                assert rc == 0, (kv, rc)
+                print(f"{path}: option {k}={v} in {(time.perf_counter() - t0) * 1e3:.0f} ms", flush=True)
+        ctxs.append((path + (f" [{env}]" if env else "") + (f" <{kern}>" if kern else "") + (f" {{{opt}}}" if opt else ""),
+                     L, cx, []))
     for rep in range(a.reps + 3):
         for path, L, cx, ms in ctxs:
             torch.cuda.synchronize()
