@@ -101,6 +101,9 @@ def parse():
                          "alone; 4 at N > 1).  A frame's tail is its costliest tiles, so a lone frame leaves the "
                          "GPU partly idle at its end; overlapping frames fill it (N = 1, --inflight 4: 4K globes "
                          "+2.5 %%, 1080p d5 +37 %%, the sphere +52 %%, profiles/r02bg_inflight_n1.txt)")
+    ap.add_argument("--chunks", type=int, default=4,
+                    help="N > 1, the single-frame phase: the frame as this many sub-frames, each gathered and assembled "
+                         "as soon as its bands are rendered, cheapest first (1 = render, then one gather, then assembly)")
     ap.add_argument("--rccl-priority", default="normal", choices=["high", "normal"],
                     help="priority of RCCL's stream (the all-gathers) relative to the render streams")
     ap.add_argument("--pool-streams", action="store_true",
@@ -519,9 +522,10 @@ def main():
     extra_steps = max(4, min(a.steps, 20))
     single = infl = None
     if multi and overlap and not a.no_extra:
-        single = single_frame_phase(a, rend, dist, D, stream, dev, slots[0], gath[0], frames[0], whole,
+        fl0 = load_flops(scene, W, H, t, depth)
+        single = single_frame_phase(a, T, rend, dist, D, stream, dev, slots[0], gath[0], frames[0], whole,
                                     (y_first, band_rows, pitch, n_bands), H, W, world, layout, band, depth,
-                                    rehearse, extra_steps)
+                                    rehearse, extra_steps, fl0["row_flops"] if fl0 else None)
     elif not multi and K == 1 and not a.no_extra:
         infl = inflight_phase(T, rend, stream, dev, frames[0], whole, H, W, depth, local, 4, extra_steps)
     if rank == 0 and a.png:
@@ -653,47 +657,109 @@ def inflight_phase(T, rend, stream, dev, frame, whole, H, W, depth, local, K, st
             "note": "throughput at the N > 1 default of 4 frames in flight: the N > 1 lines' `value` divides by this"}
 
 
-def single_frame_phase(a, rend, dist, D, stream, dev, slot, gath, frame, whole, geom, H, W, world, layout, band,
-                       depth, rehearse, steps):
+def single_frame_phase(a, T, rend, dist, D, stream, dev, slot, gath, frame, whole, geom, H, W, world, layout, band,
+                       depth, rehearse, steps, row_cost=None):
     """N > 1: one frame at a time, fully serialised (barrier + synchronize around every frame), the
-    library's kernel choice for a lone launch; events on the launch stream split each frame into
-    render / gather / assembly.  Returns the max over ranks of the mean per-step wall time and this
-    rank's event means (rank 0's in the line)."""
+    library's kernel choice for a lone launch.  Returns the max over ranks of the mean per-step wall
+    time and this rank's event means (rank 0's in the line).
+
+    --chunks C > 1 (cyclic layout): the frame is C sub-frames (distributed.chunk_plan), cheapest
+    first by the reference's per-row flop counts.  Each rank renders its bands of every chunk at once,
+    one launch per chunk on its own hardware-queue stream; chunk j's all-gather is queued on RCCL's
+    stream behind chunk j's render and its assembly behind that gather, so the cheap chunks' gathers
+    and assemblies run while the costly chunk's tail still renders.  Latency = the last chunk's
+    render end + its gather + its assembly.  C = 1: render, gather, assembly in series."""
     import torch
     y_first, band_rows, pitch, n_bands = geom
     rend.set_kernel("auto")
+    C = a.chunks if layout == "cyclic" else 1
+    plan = D.chunk_plan(H, world, band, C, row_cost) if C > 1 else [(0, H)]
+    C = len(plan)
+    rank = dist.get_rank()
+    ch = slot.shape[-1]
+    if C > 1:
+        params = [D.chunk_band_params(y0, y1, world, rank, band) for y0, y1 in plan]
+        cslots = [torch.zeros((p[4], W, ch), dtype=torch.uint8, device=dev) for p in params]
+        cgath = [torch.zeros((world * p[4], W, ch), dtype=torch.uint8, device=dev) for p in params]
+        hs = [T.HwStream(dev.index) for _ in range(C)]
+        ahs = T.HwStream(dev.index)
     rec = []
     warm = 3
     for i in range(warm + steps):
         dist.barrier()
         torch.cuda.synchronize(dev)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         t0 = time.perf_counter()
-        ev[0].record(stream)
-        rend.render_row_bands(y_first, band_rows, pitch, n_bands, slot, max_depth=depth, stream=stream)
-        ev[1].record(stream)
-        work = HostGather(gath, slot, stream) if rehearse else dist.all_gather_into_tensor(gath, slot, async_op=True)
-        work.wait()
-        ev[2].record(stream)
-        D.assemble(gath, H, world, layout, band, out=frame)
-        ev[3].record(stream)
+        if C == 1:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            ev[0].record(stream)
+            rend.render_row_bands(y_first, band_rows, pitch, n_bands, slot, max_depth=depth, stream=stream)
+            ev[1].record(stream)
+            work = HostGather(gath, slot, stream) if rehearse else dist.all_gather_into_tensor(gath, slot, async_op=True)
+            work.wait()
+            ev[2].record(stream)
+            D.assemble(gath, H, world, layout, band, out=frame)
+            ev[3].record(stream)
+            evs = {"render": [(ev[0], ev[1])], "gather": [(ev[0], ev[2])], "assemble": [(ev[0], ev[3])]}
+        else:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            works, er = [], []
+            for j, p in enumerate(params):
+                s = hs[j].torch
+                s.wait_event(e0)
+                with torch.cuda.stream(s):
+                    rend.render_row_bands(p[0], p[1], p[2], p[3], cslots[j], max_depth=depth, stream=s)
+                    e = torch.cuda.Event(enable_timing=True)
+                    e.record(s)
+                    er.append(e)
+                    works.append(HostGather(cgath[j], cslots[j], s) if rehearse else
+                                 dist.all_gather_into_tensor(cgath[j], cslots[j], async_op=True))
+            eg, ea = [], []
+            with torch.cuda.stream(ahs.torch):
+                for j, (y0, y1) in enumerate(plan):
+                    works[j].wait()                                  # the assembly stream waits for the gather
+                    e = torch.cuda.Event(enable_timing=True)
+                    e.record(ahs.torch)
+                    eg.append(e)
+                    D.assemble(cgath[j], y1 - y0, world, layout, band, out=frame[y0:y1])
+                    e = torch.cuda.Event(enable_timing=True)
+                    e.record(ahs.torch)
+                    ea.append(e)
+            evs = {"render": [(e0, e) for e in er], "gather": [(e0, e) for e in eg], "assemble": [(e0, e) for e in ea]}
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
         if i >= warm:
-            rec.append((dt, ev))
+            rec.append((dt, evs))
+    if C > 1:
+        for h in hs + [ahs]:
+            h.close()
     if not torch.equal(frame, whole):
         raise SystemExit("single-frame phase: the assembled frame differs from the single-launch render")
     wall = sum(d for d, _ in rec) / len(rec)
     e = torch.tensor([wall], dtype=torch.float64, device="cpu" if rehearse else dev)
     dist.all_reduce(e, op=dist.ReduceOp.MAX)
-    mean = lambda i, j: sum(ev[i].elapsed_time(ev[j]) for _, ev in rec) / len(rec)
-    return {"frames_in_flight": 1, "steps": steps, "ms_per_step": round(float(e.item()) * 1e3, 4),
-            "render_ms": round(mean(0, 1), 4), "gather_ms": round(mean(1, 2), 4),
-            "assemble_ms": round(mean(2, 3), 4), "frame_ms": round(mean(0, 3), 4),
-            "kernel": "library's choice (auto) for a lone launch",
-            "basis": "wall time per serialised frame (max over ranks); render/gather/assemble: rank 0's events on "
-                     "its launch stream (gather = render end -> all-gather done, incl. waiting for the slowest rank)",
-            "frame_check": "assembled frame == single-launch render, on every rank"}
+    mean = lambda k, j: round(sum(ev[k][j][0].elapsed_time(ev[k][j][1]) for _, ev in rec) / len(rec), 4)
+    out = {"frames_in_flight": 1, "steps": steps, "ms_per_step": round(float(e.item()) * 1e3, 4),
+           "chunks": C, "kernel": "library's choice (auto) for a lone launch",
+           "frame_check": "assembled frame == single-launch render, on every rank"}
+    if C == 1:
+        r, g, s = mean("render", 0), mean("gather", 0), mean("assemble", 0)
+        out.update({"render_ms": r, "gather_ms": round(g - r, 4), "assemble_ms": round(s - g, 4), "frame_ms": s,
+                    "basis": "wall time per serialised frame (max over ranks); render/gather/assemble: rank 0's events "
+                             "on its launch stream (gather = render end -> all-gather done, incl. waiting for the "
+                             "slowest rank)"})
+    else:
+        out.update({"chunk_rows": plan,
+                    "chunk_render_end_ms": [mean("render", j) for j in range(C)],
+                    "chunk_gather_done_ms": [mean("gather", j) for j in range(C)],
+                    "chunk_assembled_ms": [mean("assemble", j) for j in range(C)],
+                    "render_ms": max(mean("render", j) for j in range(C)),
+                    "frame_ms": mean("assemble", C - 1),
+                    "basis": "wall time per serialised frame (max over ranks); chunk_*: rank 0's events, ms from the "
+                             "frame's start: each chunk's render end (its stream), all-gather done and assembly done "
+                             "(the assembly stream), chunks cheapest first"})
+        out["last_chunk_gather_ms"] = round(out["chunk_gather_done_ms"][-1] - out["chunk_render_end_ms"][-1], 4)
+    return out
 
 
 class HostGather:
@@ -767,6 +833,25 @@ def launcher_check(a, json_out):
         dist.all_gather_into_tensor(gath, slot)
         frame = D.assemble(gath, H, world, layout, band)
         ok = ok and torch.equal(frame, pattern(range(H)))
+    # the single-frame phase's chunks (distributed.chunk_plan): each sub-frame's bands gathered and
+    # assembled on their own, in a cost order that is not the frame order
+    chunks_ok = None
+    if layout == "cyclic" and a.chunks > 1:
+        plan = D.chunk_plan(H, world, band, a.chunks, row_cost=[(y * 7919) % 101 for y in range(H)])
+        frame = torch.zeros((H, W, 4), dtype=torch.uint8)
+        for y0, y1 in plan:
+            f0, br, bp, nb, srows = D.chunk_band_params(y0, y1, world, rank, band)
+            cslot = torch.zeros((srows, W, ch), dtype=torch.uint8)
+            cys = [f0 + (r // br) * bp + r % br for r in range(br * nb)]
+            ck = [r for r, y in enumerate(cys) if y < y1]
+            if ck:
+                cslot[ck] = pattern([cys[r] for r in ck], ch)
+            cg = torch.empty((world * srows, W, ch), dtype=torch.uint8)
+            dist.all_gather_into_tensor(cg, cslot)
+            D.assemble(cg, y1 - y0, world, layout, band, out=frame[y0:y1])
+        chunks_ok = len(plan) > 1 and sorted(plan) == [(c[0], c[1]) for c in sorted(plan)] and \
+            torch.equal(frame, pattern(range(H)))
+        ok = ok and chunks_ok
     flags = [None] * world
     dist.all_gather_object(flags, (ok, len(keep)))
     if rank == 0:
@@ -774,7 +859,8 @@ def launcher_check(a, json_out):
                 "n_gpus": world, "steps": a.steps, "warmup": 0,
                 "distributed": {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(),
                                 "rows_per_rank": [n for _, n in flags], "layout": layout, "band_rows": band,
-                                "gather": a.gather, "frame_check": all(f for f, _ in flags)},
+                                "gather": a.gather, "frame_check": all(f for f, _ in flags),
+                                "chunks": a.chunks if chunks_ok is not None else 1, "chunks_check": chunks_ok},
                 "config": {"width": W, "height": H}}
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()

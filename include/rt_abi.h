@@ -277,10 +277,15 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  * rt_ctx_upload (or here, when a scene is already uploaded): seconds of host time per new scene (the
  * code object is cached per process by the program text), so it pays for hosts that render many
  * frames of one scene.  Launches whose kernel has no specialised form (wavefront, refraction
- * deferred, RT_OPT_FAST_CLAMP 0 on a min/max-clamp scene) keep the generic kernels. */
+ * deferred, RT_OPT_FAST_CLAMP 0 on a min/max-clamp scene) keep the generic kernels.
+ * RT_OPT_TAIL_TILES: tail-bound launches of scenes without a transparent object (the deferred
+ * kernel's ordered launches, RGBA8 / RGB8) take their costliest calibrated tiles out of the main
+ * launch and render them in a kernel of their own, started first on an internal stream with a
+ * hardware queue of its own, several lanes tracing each pixel's rays together; this many tiles
+ * (default 64, at most an eighth of the launch's; 0: none).  Same pixels. */
 typedef enum rt_option {
   RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4,
-  RT_OPT_WAVEFRONT_PAIRS = 5, RT_OPT_SPECIALIZE = 6
+  RT_OPT_WAVEFRONT_PAIRS = 5, RT_OPT_SPECIALIZE = 6, RT_OPT_TAIL_TILES = 7
 } rt_option;
 typedef enum rt_kernel_choice {
   RT_KERNEL_AUTO = 0, RT_KERNEL_MEGA = 1, RT_KERNEL_DEFERRED = 2, RT_KERNEL_WAVEFRONT = 3

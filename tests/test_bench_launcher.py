@@ -34,6 +34,15 @@ def test_self_launch_gloo(world, layout, gather):
     assert d["world_size_seen"] == world and d["backend"] == "gloo" and d["gather"] == gather
     assert d["frame_check"] is True
     assert len(d["rows_per_rank"]) == world and sum(d["rows_per_rank"]) == line["config"]["height"]
+    if layout == "cyclic":                          # the single-frame phase's chunked gathers (default 4)
+        assert d["chunks"] == 4 and d["chunks_check"] is True
+
+
+def test_self_launch_gloo_chunks():
+    """Sub-frame gathers at other chunk counts, world 3 (a partial last slot band)."""
+    for c in (2, 3):
+        d = _run("--gpus", "3", "--launcher-check", "--layout", "cyclic", "--steps", "1", "--chunks", str(c))["distributed"]
+        assert d["frame_check"] is True and d["chunks"] == c and d["chunks_check"] is True
 
 
 def test_host_cpus_reports_usable_cores():

@@ -38,6 +38,19 @@ render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_p
                                     &win);
 }
 
+// The tail kernel (rt_device.h tail_body): the costliest tiles of a tail-bound launch, G lanes per pixel.
+// A few thousand waves at most, whose latency is the point: 2 waves/SIMD, so nothing spills.
+#ifndef RT_WAVES_PER_EU_TAIL
+#define RT_WAVES_PER_EU_TAIL 2
+#endif
+template <bool F64, bool FC, int G>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_TAIL))) void
+render_tail_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth,
+                   uint8_t* __restrict__ out, size_t stride, const int32_t* __restrict__ tiles, int rgb) {
+  __shared__ double s_frames[rows_lds_doubles<RT_MODE_REFL>()];
+  tail_body<F64, FC, G>(S, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, tiles, rgb, (lds_f64*)s_frames);
+}
+
 }  // namespace
 
 using namespace rt;
@@ -202,6 +215,34 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   if (c->spec_mod && mode == c->spec_mode && fc == c->spec_fc)
     sfn = deferred ? c->spec_def[f64 ? 1 : 0][calibrate ? 1 : 0] : c->spec_rows[f64 ? 1 : 0][calibrate ? 1 : 0];
   c->last_kernel = deferred ? (sfn ? "deferred (specialised)" : "deferred") : (sfn ? "megakernel (specialised)" : "megakernel");
+  // the tail kernel first, on its own hardware queue, concurrently with the main launch (which then
+  // waits for it on the caller's stream): the costliest tiles' chains start at once, G lanes per pixel
+  const bool tail = order && deferred && slot->n_tail > 0;
+  if (tail) {
+    if (!c->tail_stream) {
+      hipDeviceProp_t prop;
+      RT_HIP(hipGetDeviceProperties(&prop, c->device));
+      std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0xFFFFFFFFu);
+      if (prop.multiProcessorCount % 32) mask.back() = (1u << (prop.multiProcessorCount % 32)) - 1u;
+      RT_HIP(hipExtStreamCreateWithCUMask(&c->tail_stream, (uint32_t)mask.size(), mask.data()));
+      RT_HIP(hipEventCreateWithFlags(&c->tail_ev0, hipEventDisableTiming));
+      RT_HIP(hipEventCreateWithFlags(&c->tail_ev1, hipEventDisableTiming));
+    }
+    RT_HIP(hipEventRecord(c->tail_ev0, st));
+    RT_HIP(hipStreamWaitEvent(c->tail_stream, c->tail_ev0, 0));
+    const int nl = c->dev.n_leaves;
+    const int G = nl <= 16 ? 16 : nl <= 32 ? 32 : 64;
+    const dim3 tg(slot->n_tail * (unsigned)G);
+    hipStream_t ts = c->tail_stream;
+#define RT_LAUNCH_TAIL(FCv, Gv) hipLaunchKernelGGL((render_tail_kernel<false, FCv, Gv>), tg, dim3(64), 0, ts, c->dev, a0, a1, a2, a3, \
+                                                   max_depth, target, tstride, slot->d_tail, rgbi)
+    if (fc) { if (G == 16) RT_LAUNCH_TAIL(true, 16); else if (G == 32) RT_LAUNCH_TAIL(true, 32); else RT_LAUNCH_TAIL(true, 64); }
+    else { if (G == 16) RT_LAUNCH_TAIL(false, 16); else if (G == 32) RT_LAUNCH_TAIL(false, 32); else RT_LAUNCH_TAIL(false, 64); }
+#undef RT_LAUNCH_TAIL
+    RT_HIP(hipGetLastError());
+    RT_HIP(hipEventRecord(c->tail_ev1, ts));
+    c->last_kernel = sfn ? "tail + deferred (specialised)" : "tail + deferred";
+  }
   if (sfn) {
     void* kargs[] = {&c->dev, (void*)&a0, (void*)&a1, (void*)&a2, (void*)&a3, &max_depth, &target, &tstride,
                      (void*)&order, &cost, (void*)&rgbi};
@@ -220,6 +261,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
 #undef RT_LAUNCH_ROWS
 #undef RT_LAUNCH_DEFERRED
   RT_HIP(hipGetLastError());
+  if (tail) RT_HIP(hipStreamWaitEvent(st, c->tail_ev1, 0));
   if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
   c->timed = c->timing;
   if (tune) {                         // synchronous, once per ray-tree geometry (see above)
@@ -269,22 +311,31 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
       std::vector<uint32_t> sorted_cost(h_cost);
       std::nth_element(sorted_cost.begin(), sorted_cost.begin() + n_tiles / 2, sorted_cost.end());
       const double med = std::max(1.0, (double)sorted_cost[n_tiles / 2]);
+      // the costliest tiles go to the tail kernel (reflection-only scenes, RGBA8 / RGB8 launches): at most
+      // an eighth of the launch, never the whole launch
+      size_t n_tail = 0;
+      if (!refr && !f64 && c->tail_tiles > 0 && n_tiles >= 16) {
+        n_tail = std::min<size_t>((size_t)c->tail_tiles, n_tiles / 8);
+        RT_HIP(hipMalloc((void**)&slot->d_tail, n_tail * sizeof(int32_t)));
+        RT_HIP(hipMemcpy(slot->d_tail, h_order.data(), n_tail * sizeof(int32_t), hipMemcpyHostToDevice));
+        slot->n_tail = (uint32_t)n_tail;
+      }
       std::vector<int32_t> split;
       split.reserve(n_tiles + n_tiles / 8);
-      for (size_t i = 0; i < n_tiles; ++i) {
+      for (size_t i = n_tail; i < n_tiles; ++i) {
         const uint32_t t = (uint32_t)h_order[i];
         int lp = 0;
         while (lp < RT_SPLIT_MAX_LOG2 && h_cost[t] >= split_k * med * (double)(2 << lp)) ++lp;
         for (int part = 0; part < (1 << lp); ++part)
           split.push_back((int32_t)(t | ((uint32_t)part << 20) | ((uint32_t)lp << 24)));
       }
-      if (split.size() > n_tiles) {
+      if (split.size() > n_tiles) {                 // more entries than the calibration's table holds
         int32_t* d = nullptr;
         RT_HIP(hipMalloc((void**)&d, split.size() * sizeof(int32_t)));
         (void)hipFree(slot->d_order);
         slot->d_order = d;
-        h_order.swap(split);
       }
+      h_order.swap(split);
     }
     slot->grid = (uint32_t)h_order.size();
     RT_HIP(hipMemcpyAsync(slot->d_order, h_order.data(), h_order.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));

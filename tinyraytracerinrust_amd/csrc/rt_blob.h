@@ -85,7 +85,8 @@ struct alignas(16) RtLeaf {
   int32_t prog_end;
   int32_t n_lit;        // >= 0: the filter program is the conjunction of n_lit literals below
   int32_t lit[RT_MAX_LITS];   // literal = 2 * leaf + want: leaf[lit >> 1].is_inside(p) == (lit & 1)
-  int32_t pad0[3];
+  int32_t object;       // the top-level object this leaf belongs to (the cooperative tail walk, rt_device.h)
+  int32_t pad0[2];
   double blo[3], bhi[3];// culling box of this leaf's accepted hits (own bound ^ required-inside siblings)
   double inv[12];       // inverse matrix rows 0..2 (row-major, 4 per row)
   double inv_o[3];      // transform_vector((0,0,0), inverse)   (transformation.rs:80-83)

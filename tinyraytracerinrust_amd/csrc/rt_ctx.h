@@ -57,6 +57,8 @@ struct rt_ctx {
     bool deferred = false;            // ordered launches take the deferred-shadow kernel
     int wf_tune = 0;                  // ray-tree scenes, RT_KERNEL_AUTO: 0 not yet timed, 1 megakernel, 2 wavefront
     bool valid = false;               // set once the sorted order is on the device
+    int32_t* d_tail = nullptr;        // deferred launches of reflection-only scenes: the costliest tiles, rendered by
+    uint32_t n_tail = 0;              //   the tail kernel (G lanes per pixel) on tail_stream, not by the main launch
   };
   static constexpr int RT_ORDER_SLOTS = 8;
   OrderSlot order[RT_ORDER_SLOTS];
@@ -75,6 +77,9 @@ struct rt_ctx {
   uint64_t spec_hash = 0;               // FNV-1a of the program text (the code-object cache key)
   double spec_compile_ms = 0.0;         // 0 when the code object came from the process cache
   const char* last_kernel = "none";     // what the last row launch ran (rt_ctx_kernel_info)
+  int tail_tiles = 64;                  // rt_ctx_set_option(RT_OPT_TAIL_TILES): tiles the tail kernel takes (0: none)
+  hipStream_t tail_stream = nullptr;    // the tail kernel's stream (a hardware queue of its own), made on first use
+  hipEvent_t tail_ev0 = nullptr, tail_ev1 = nullptr;
 };
 
 using rt::fail;

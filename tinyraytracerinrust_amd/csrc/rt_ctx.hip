@@ -23,6 +23,7 @@ bool diag_env(const char* name) {
 void drop_order(rt_ctx::OrderSlot& s) {
   if (s.d_order) (void)hipFree(s.d_order);     // hipFree waits for work that may still read it
   if (s.d_cost) (void)hipFree(s.d_cost);
+  if (s.d_tail) (void)hipFree(s.d_tail);
   s = rt_ctx::OrderSlot();
 }
 void drop_orders(rt_ctx* c) {
@@ -188,6 +189,15 @@ int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
     c->timed = false;                  // no launch recorded under the new setting yet
     return RT_OK;
   }
+  if (option == RT_OPT_TAIL_TILES) {
+    if (value < 0 || value > 4096) return fail(RT_ERR_INVALID, "RT_OPT_TAIL_TILES %d not in [0, 4096]", value);
+    if (value != c->tail_tiles) {
+      RT_HIP(hipSetDevice(c->device));
+      drop_orders(c);                            // the tail set is chosen at calibration
+      c->tail_tiles = value;
+    }
+    return RT_OK;
+  }
   if (option == RT_OPT_SPECIALIZE) {
     if (value < 0 || value > 2) return fail(RT_ERR_INVALID, "RT_OPT_SPECIALIZE value %d", value);
     if (value == c->spec_on) return RT_OK;
@@ -271,6 +281,9 @@ void rt_ctx_free(rt_ctx* c) {
   if (c->wfp) (void)hipFree(c->wfp);
   drop_orders(c);
   rt::spec_drop(c);
+  if (c->tail_stream) (void)hipStreamDestroy(c->tail_stream);
+  if (c->tail_ev0) (void)hipEventDestroy(c->tail_ev0);
+  if (c->tail_ev1) (void)hipEventDestroy(c->tail_ev1);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->tev0) (void)hipEventDestroy(c->tev0);

@@ -754,6 +754,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
     if (err) return err;
     ob.node_count = (int32_t)f.nodes.size() - ob.node_begin;
     ob.leaf_count = (int32_t)f.leaves.size() - ob.leaf_begin;
+    for (int32_t l = ob.leaf_begin; l < ob.leaf_begin + ob.leaf_count; ++l) f.leaves[l].object = (int32_t)f.objects.size();
     if (ob.node_count > 32) return fail(RT_ERR_UNSUPPORTED, "object with %d CSG nodes (max 32)", ob.node_count);
     // Hit-filter program per leaf: for every CSG ancestor, the sibling's is_inside test with
     // the polarity of csg.rs:43-95 (Union: !in, !in; Intersection: in, in; Difference: !in, in).

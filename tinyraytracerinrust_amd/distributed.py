@@ -57,6 +57,33 @@ def band_params(height: int, world: int, rank: int, layout: str, band: int) -> T
     return own[0][0], band, world * band, len(own)
 
 
+def chunk_plan(height: int, world: int, band: int, chunks: int, row_cost=None) -> List[Tuple[int, int]]:
+    """Split a cyclic-band frame into `chunks` sub-frames that gather independently: slot band s of
+    every rank covers frame rows [s * world * band, (s + 1) * world * band), so a run of slot bands
+    is a contiguous frame row range with the same cyclic layout inside it (its own render launch per
+    rank, its own all-gather of world x its slot rows, its own assembly into frame rows [Y0, Y1)).
+    Returns [(Y0, Y1)] in the order to render and gather them: cheapest first when per-row costs are
+    given (the costly tail then renders while the cheap chunks' gathers run), else frame order."""
+    span = world * band
+    nsb = -(-height // span)                       # slot bands per rank (the last may be partial)
+    chunks = max(1, min(chunks, nsb))
+    cuts = [round(i * nsb / chunks) for i in range(chunks + 1)]
+    plan = [(cuts[i] * span, min(height, cuts[i + 1] * span)) for i in range(chunks) if cuts[i + 1] > cuts[i]]
+    if row_cost is not None:
+        plan.sort(key=lambda c: sum(row_cost[c[0]:c[1]]))
+    return plan
+
+
+def chunk_band_params(y0: int, y1: int, world: int, rank: int, band: int) -> Tuple[int, int, int, int, int]:
+    """(y_first, band_rows, band_pitch, n_bands, slot_rows) of this rank's bands in frame rows [y0, y1)
+    of a chunk_plan chunk; slot_rows = the chunk's (equal, padded) rows per rank."""
+    span = world * band
+    nsb = -(-(y1 - y0) // span)
+    first = y0 + rank * band
+    n = len(range(first, y1, span))
+    return first, band, span, n, nsb * band
+
+
 def render_local(render_rows: Callable[[int, int, torch.Tensor], None], height: int, width: int, world: int,
                  rank: int, layout: str, band: int, device, dtype=torch.uint8) -> torch.Tensor:
     """This rank's slot: its rows packed densely (padding rows left zero)."""

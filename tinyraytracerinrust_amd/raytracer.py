@@ -346,6 +346,11 @@ class Renderer:
         2 its f64 and calibration kernels too."""
         check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_SPECIALIZE, int(level)))
 
+    def set_tail_tiles(self, tiles: int = 64) -> None:
+        """rt_ctx_set_option(RT_OPT_TAIL_TILES): tiles a tail-bound launch of a reflection-only scene hands to
+        the tail kernel (several lanes per pixel, its own hardware queue); 0 none (same pixels)."""
+        check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_TAIL_TILES, int(tiles)))
+
     def kernel_info(self) -> str:
         """rt_ctx_kernel_info: generic or scene-specialised kernels, and what the last row launch ran."""
         buf = ctypes.create_string_buffer(512)

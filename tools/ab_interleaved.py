@@ -29,7 +29,7 @@ def main():
                          "the burst's wall time / burst")
     ap.add_argument("--upload-env", nargs="*", default=[],
                     help="per library (in order): KEY=VAL set in the environment while its scene is compiled and "
-                         "uploaded (host-side flattening switches, e.g. RT_NO_LIT_ORDER=1); '-' for none")
+                         "uploaded (host-side flattening switches of a `make diag DIAG=-DRT_DIAG_ENV` build, e.g. RT_NO_LIT_ORDER=1); '-' for none")
     ap.add_argument("--check", action="store_true",
                     help="after timing, render once more per library and require every frame to equal the first's")
     ap.add_argument("--kernel", nargs="*", default=[],

@@ -28,11 +28,14 @@ def main():
     ap.add_argument("--same-ctx", action="store_true", help="one context (one calibration) for every repetition")
     ap.add_argument("--streams", default="hw", choices=["hw", "pool"],
                     help="hw: rt_stream_create (a hardware queue each, as bench.py); pool: torch.cuda.Stream()")
+    ap.add_argument("--options", nargs="*", default=["-"],
+                    help="context option sets to compare, each OPT=VAL[,OPT=VAL] by number (rt_abi.h rt_option: 6 = "
+                         "RT_OPT_SPECIALIZE, 7 = RT_OPT_TAIL_TILES); '-' for none")
     a = ap.parse_args()
     import torch
     W, H = 3840, 2160
     text = open(os.path.join(S, "globes.scene")).read().encode()
-    for path in a.libs:
+    for path, opts in [(p, o) for p in a.libs for o in a.options]:
         L = ctypes.CDLL(os.path.abspath(path))
         for n in (int(v) for v in a.ns.split(",")):
             band = 8
@@ -63,6 +66,10 @@ def main():
                     streams = fixed if a.fixed_streams else new_streams()
                     mode = ("auto" if k == 1 else "mega") if a.kernel == "bench" else a.kernel
                     assert L.rt_ctx_set_option(cx, 0, {"auto": 0, "mega": 1, "deferred": 2, "wavefront": 3}[mode]) == 0   # RT_OPT_KERNEL
+                    if opts != "-":
+                        for kv in opts.split(","):
+                            o, v = (int(x) for x in kv.split("="))
+                            assert L.rt_ctx_set_option(cx, o, v) == 0, kv
 
                     def issue(i):
                         s = streams[i % k]
@@ -83,7 +90,7 @@ def main():
                     if not a.same_ctx:
                         L.rt_ctx_free(cx)
                         L.rt_scene_free(sc)
-                    print(f"N={n} K={k}: {' '.join(f'{v:.4f}' for v in res)} ms per frame share, {mode} kernel, {a.streams} streams  ({path})",
+                    print(f"N={n} K={k}: {' '.join(f'{v:.4f}' for v in res)} ms per frame share, {mode} kernel, {a.streams} streams, options {opts}  ({path})",
                           flush=True)
 
 
