@@ -247,7 +247,7 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  *     streams (their launches overlap, so no launch's tail leaves the GPU idle);
  *   RT_KERNEL_DEFERRED: always the deferred-shadow kernel (scenes whose rays form chains);
  *   RT_KERNEL_WAVEFRONT: the launch-wide wavefront path for any scene: one pass per recursion depth
- *     over a dense queue of that depth's rays, then a bottom-up fold (render_kernels.hip wf_*).
+ *     over a dense queue of that depth's rays, then a bottom-up fold (k_wavefront.hip wf_*).
  * Changing the kernel drops the context's tile orders (the next launch of each geometry
  * calibrates again).  Scenes with a transparent object always take the refraction megakernel.
  * RT_OPT_TIMING: 1 (default) records a HIP event pair around every render launch for
@@ -276,7 +276,8 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  * and calibration launches too.  The compile runs on the calling thread at
  * rt_ctx_upload (or here, when a scene is already uploaded): seconds of host time per new scene (the
  * code object is cached per process by the program text), so it pays for hosts that render many
- * frames of one scene.  Launches whose kernel has no specialised form (wavefront, refraction
+ * frames of one scene.  Scenes of more than 32 objects or 48 leaves keep the generic kernels (the
+ * unrolled walks grow with the scene; rt_ctx_kernel_info says so).  Launches whose kernel has no specialised form (wavefront, refraction
  * deferred, RT_OPT_FAST_CLAMP 0 on a min/max-clamp scene) keep the generic kernels.
  * RT_OPT_TAIL_TILES: tail-bound launches of scenes without a transparent object (the deferred
  * kernel's ordered launches, RGBA8 / RGB8) take their costliest calibrated tiles out of the main

@@ -62,7 +62,7 @@ def _primitive(r, name):
 
 def random_scene(seed: int, chains: bool = False) -> str:
     """chains=True: transparent objects get reflectivity 0, so the scene's rays form chains (the
-    refraction chain kernels: render_kernels.hip RT_MODE_CHAIN and the deferred REFR path)."""
+    refraction chain kernels: rt_device.h trace, RT_MODE_CHAIN and the deferred REFR path)."""
     _CHAINS[0] = chains
     try:
         return _random_scene(seed)

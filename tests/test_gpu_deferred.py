@@ -1,4 +1,4 @@
-"""The deferred-shadow path (render_kernels.hip trace_deferred: chain phase, wave-wide shadow
+"""The deferred-shadow path (rt_device.h trace_deferred: chain phase, wave-wide shadow
 phase through an LDS window, post-order fold) on EVERY tile -- rt_ctx_set_option(RT_OPT_KERNEL,
 RT_KERNEL_DEFERRED) -- against the oracle (src/raytracer/raytracer.rs:132-287): small frames (no
 ordered launch, lanes outside the frame trace other lanes' shadow rays) and ordered frames whose

@@ -1,4 +1,4 @@
-"""The min/max colour clamps (render_kernels.hip in_limit<FC>, taken when rt::flatten proves every
+"""The min/max colour clamps (rt_device.h in_limit<FC>, taken when rt::flatten proves every
 colour-op operand finite and >= +0) against the compare/select clamps of color.rs:36-53 as the
 reference writes them: the f64 colours of whole frames must be BIT-identical.  The two forms are
 selected per context with rt_ctx_set_option(RT_OPT_FAST_CLAMP)."""

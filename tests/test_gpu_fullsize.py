@@ -12,7 +12,7 @@ src/raytracer/raytracer.rs:132-287 and its callees) on all usable host cores.
 
 Bar: RGBA8 bit-identical (the north star's 1-LSB bound is reported, the count of differing channels
 printed on failure).  These pin the exactness of
-the kernels' culling (render_kernels.hip "conservative culling") over whole frames.
+the kernels' culling (rt_device.h "conservative culling") over whole frames.
 """
 import numpy as np
 import pytest

@@ -79,13 +79,13 @@ def test_globes1080_d5_specialised(worldmap, kernel):
         assert_close(f.cpu().numpy(), None, ref, None, f"spec 1080p d5 {kernel} ({r.kernel_info()})")
 
 
-@pytest.mark.parametrize("name,t,W,H,depth", [("spinning_globes", 0.3, 640, 480, 10), ("fractal", 0.0, 320, 240, 10),
-                                              ("three_cubes", 0.0, 320, 240, 10), ("spinning_gimbals", 0.4, 320, 240, 10),
-                                              ("ground_star", 0.2, 320, 240, 10)])
+@pytest.mark.parametrize("name,t,W,H,depth", [("spinning_globes", 0.3, 640, 480, 10), ("three_cubes", 0.0, 320, 240, 10),
+                                              ("spinning_gimbals", 0.4, 320, 240, 10), ("ground_star", 0.2, 320, 240, 10),
+                                              ("spinning_cube", 0.3, 320, 240, 10)])
 def test_reference_scenes_specialised_level2(worldmap, name, t, W, H, depth):
     """Level 2: every row launch specialised (calibration, ordered, f64), against the oracle in RGBA8,
-    and the f64 colours bit-equal to the generic kernels' -- refraction chains (spinning_globes), ray
-    trees (fractal), cubes, CSG gimbals."""
+    and the f64 colours bit-equal to the generic kernels' -- refraction chains (spinning_globes), cubes,
+    CSG gimbals and stars."""
     import tinyraytracerinrust_amd as T
     text = scene_text(name)
     rt, r = _renderer(text, t, W, H, depth, 2)
@@ -102,17 +102,33 @@ def test_reference_scenes_specialised_level2(worldmap, name, t, W, H, depth):
     assert same.all(), f"{name}: {int((~same).sum())} f64 channels differ from the generic kernels"
 
 
-def test_fuzz_scenes_specialised(worldmap):
+@pytest.mark.parametrize("seed", [11, 23, 37, 3001, 3002])
+def test_fuzz_scenes_specialised(worldmap, seed):
     """Random scenes of the parity fuzz suite (tests/scene_fuzz.py): nested CSG, tilted planes,
-    transparent objects, colours outside [0, 1], random transforms and lights."""
+    transparent objects, colours outside [0, 1], random transforms and lights (3001+: thin rotated rods
+    and slabs with oriented boxes)."""
     from tests.scene_fuzz import random_scene, random_rod_scene
     W, H = 96, 72
-    for seed, text in [(s, random_scene(s)) for s in (11, 23, 37)] + [(s, random_rod_scene(s)) for s in (3001, 3002)]:
-        rt, r = _renderer(text, 0.0, W, H, 6, 2)
-        su = r.render_rows_host(0, H)
-        sf = r.render_rows_host(0, H, f64=True)
-        rf, ru = _oracle(text, 0.0, W, H, 6, f64=True)
-        assert_close(su, sf, ru, rf, f"spec fuzz seed {seed}")
+    text = random_rod_scene(seed) if seed >= 3000 else random_scene(seed)
+    rt, r = _renderer(text, 0.0, W, H, 6, 2)
+    su = r.render_rows_host(0, H)
+    sf = r.render_rows_host(0, H, f64=True)
+    rf, ru = _oracle(text, 0.0, W, H, 6, f64=True)
+    assert_close(su, sf, ru, rf, f"spec fuzz seed {seed}")
+
+
+def test_large_scene_keeps_generic_kernels(worldmap):
+    """fractal.scene (171 objects) is beyond the unrolling limits: the option leaves the generic kernels
+    in place, says so, and the frame is unchanged."""
+    import tinyraytracerinrust_amd as T
+    W, H = 96, 72
+    rt = T.RayTracer(W, H)
+    rt.load_scene(scene_text("fractal"), 0.0, asset_dir=SCENES)
+    r = rt.renderer
+    a = r.render_rows_host(0, H)
+    r.set_specialize(1)
+    assert r.kernel_variant() == "generic" and "too large to specialise" in r.kernel_info()
+    assert np.array_equal(a, r.render_rows_host(0, H))
 
 
 def test_specialise_option_round_trip(worldmap):

@@ -1,4 +1,4 @@
-"""The launch-wide wavefront path (render_kernels.hip wf_trace_kernel / wf_fold_kernel /
+"""The launch-wide wavefront path (k_wavefront.hip wf_trace_kernel / wf_fold_kernel /
 wf_fixup_kernel; rt_ctx_set_option(RT_OPT_KERNEL, RT_KERNEL_WAVEFRONT)): one pass per recursion
 depth over a dense queue of that depth's rays, then the bottom-up fold of raytracer.rs:256-279.
 Every frame against the oracle (src/raytracer/raytracer.rs:132-287): reflection chains, refraction

@@ -706,7 +706,7 @@ extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const u
                                        const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit,
                                        hipStream_t stream);
 
-// Pair-path arrays (render_kernels.hip "wavefront pair path"): per ray of a level (R = the larger of
+// Pair-path arrays (above, "wavefront pair path"): per ray of a level (R = the larger of
 // the pixel slots and the level capacity) and, grow-only, the pair lists for `need` pairs.
 static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t lcap, size_t need, WfPairs* P) {
   const size_t nl = (size_t)std::max(1, c->dev.n_lights);

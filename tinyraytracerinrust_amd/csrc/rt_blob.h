@@ -1,5 +1,5 @@
 // rt_blob.h -- the flattened, immutable scene as it lives in HBM (shared by the host
-// flattener, scene_flatten.cpp, and the gfx950 kernels, render_kernels.hip).
+// flattener, scene.cpp, and the gfx950 kernels, rt_device.h).
 //
 // Design (DESIGN.md "Data layout in HBM"):
 //  * The reference walks a tree of boxed trait objects per ray (RTObject -> dyn MathShape
@@ -114,7 +114,7 @@ struct alignas(16) RtLeaf {
 // n_a * v_a != 0 (the other two products are signed zeros); when n_a * v_a is +-0 the sum is some
 // +-0 too.  The plane test only asks `v_d != 0` of the direction term and, for traversals (t > EPS
 // wanted), the strict signs of num = dot(pnorm, o) + d and v_d, which a signed zero never passes,
-// so the short form decides every traversal test exactly (render_kernels.hip leaf_candidates).
+// so the short form decides every traversal test exactly (rt_device.h leaf_candidates).
 // Literal form: most CSG filters (every ancestor requiring an intersection / difference sibling
 // inside, or a union sibling outside) are a plain conjunction of single-leaf is_inside tests;
 // the host rewrites the postfix program into at most RT_MAX_LITS literals (n_lit = -1: keep the
@@ -164,7 +164,7 @@ struct alignas(16) RtTrav {
   int32_t obj;                      // >= 0: object index; -1: group node
   int32_t skip;                     // node index after this node's subtree
   int32_t cull;                     // object node: a copy of RtObject::cull (one record per step of a
-  int32_t shadow_skip;              //   per-lane walk, render_kernels.hip wfp_cand_kernel), ::shadow_skip
+  int32_t shadow_skip;              //   per-lane walk, k_wavefront.hip wfp_cand_kernel), ::shadow_skip
 };
 
 struct RtTexture {
@@ -194,7 +194,7 @@ struct RtDevScene {
   int32_t width, height;
   int32_t any_transparent;          // some object has transparency != 0 (refraction possible)
   int32_t shadow_early_out;         // every transparency is finite: product==0 stays 0
-  int32_t colour_fast;              // colour clamps may take the min/max form (render_kernels.hip FC)
+  int32_t colour_fast;              // colour clamps may take the min/max form (rt_device.h FC)
   int32_t ray_chains;               // every hit spawns at most one ray (scene.cpp flatten)
   int32_t shadow_pow;               // a shadow product depends only on its factors' multiset: every
                                     // transparency is finite and all those other than +-0 and 1 are

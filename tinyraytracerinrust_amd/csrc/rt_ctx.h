@@ -70,6 +70,7 @@ struct rt_ctx {
   int spec_mode = 0;                    // RT_MODE_* of the uploaded scene
   bool spec_fc = false;                 // the program's clamp form (RtDevScene::colour_fast)
   bool spec_deferred = false;           // the program also holds the deferred kernels
+  bool spec_fits = false;               // small enough to specialise (RT_SPEC_MAX_OBJECTS / _LEAVES)
   hipModule_t spec_mod = nullptr;       // non-null once the kernels are loaded (null: generic kernels)
   hipModule_t spec_mods[8] = {};        // one module per specialised kernel, on this context's device
   hipFunction_t spec_rows[2][2] = {};   // [f64][cal]
@@ -89,6 +90,9 @@ using rt::fail;
     hipError_t e_ = (call);                                                            \
     if (e_ != hipSuccess) return fail(RT_ERR_DEVICE, "%s failed: %s", #call, hipGetErrorString(e_)); \
   } while (0)
+
+#define RT_SPEC_MAX_OBJECTS 32
+#define RT_SPEC_MAX_LEAVES 48
 
 namespace rt {
 // rt_ctx.hip

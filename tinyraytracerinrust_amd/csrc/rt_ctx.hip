@@ -167,6 +167,9 @@ int rt_ctx_kernel_info(rt_ctx* c, char* buf, size_t cap) {
     snprintf(s, sizeof s, "scene-specialised (hipRTC %016llx, %s, compiled in %.0f ms)%s; last launch: %s",
              (unsigned long long)c->spec_hash, c->spec_mode == RT_MODE_REFL ? "reflection" : c->spec_mode == RT_MODE_CHAIN ? "chain" : "tree",
              c->spec_compile_ms, c->spec_compile_ms == 0.0 ? " [process cache]" : "", c->last_kernel);
+  else if (c->spec_on && c->uploaded && !c->spec_fits)
+    snprintf(s, sizeof s, "generic (librt_mi355x.so; scene too large to specialise: > %d objects or > %d leaves); last "
+             "launch: %s", RT_SPEC_MAX_OBJECTS, RT_SPEC_MAX_LEAVES, c->last_kernel);
   else
     snprintf(s, sizeof s, "generic (librt_mi355x.so); last launch: %s", c->last_kernel);
   snprintf(buf, cap, "%s", s);

@@ -21,7 +21,7 @@
 // Operations whose operand ranges rt_acos guarantees (|x| < 1 branches): sqrt of z in
 // (2^-54, 1/4], p / q with p in (2^-120, 1) and q in [1/2, 1], and the residual quotient
 // fma(-s,s,z) / 2s (numerator 0 or |.| >= 2^-160).  The device build substitutes cores without the
-// scaling steps that are identities on those ranges (render_kernels.hip: bit-identical results).
+// scaling steps that are identities on those ranges (rt_device.h: bit-identical results).
 #ifndef RT_SQRT_IN_RANGE
 #define RT_SQRT_IN_RANGE(x) sqrt(x)
 #endif

@@ -276,7 +276,7 @@ static Box leaf_box(const ShapeRec& s) {
     r.lo[i] = (double)(wc - half[i] - margin);
     r.hi[i] = (double)(wc + half[i] + margin);
     // the kernel's slab arithmetic is only proven conservative for coordinates within 1e6
-    // (render_kernels.hip cull_ray): larger boxes are never culled
+    // (rt_device.h cull_ray): larger boxes are never culled
     if (!(fabs(r.lo[i]) <= RT_CULL_COORD_MAX) || !(fabs(r.hi[i]) <= RT_CULL_COORD_MAX)) return box_infinite();
   }
   return r;
@@ -391,7 +391,7 @@ static int filter_literals(const std::vector<RtProg>& prog, int32_t b, int32_t e
 }
 
 // Concentric sphere leaves with one transform share their ray terms (rt_blob.h share_prev).  The
-// refraction kernels use the shared terms (render_kernels.hip trace: SHARE), so in scenes with a
+// refraction kernels use the shared terms (rt_device.h trace: SHARE), so in scenes with a
 // transparent object per-leaf box tests that cannot cull, or that cost what the shared quadratic
 // costs, are dropped as well.  `uncond`: the leaf is evaluated whenever its object is entered.
 static void share_sphere_terms(FlatScene& f, RtObject* ob) {
@@ -477,7 +477,7 @@ static void order_literals(FlatScene& f, const RtObject& ob) {
 // inv, inv_o, c): the filter's point q = xf(inv, o + t d) lies at |q - c| = r_X up to rounding in
 // the quadratic's t, the world point and the transform, all below ~1e-14 (1 + |M|) (|o| + |p| +
 // |T| + |c| + r) -- |p| is bounded by the sphere's world extent, and the traversals only skip the
-// filter for ray origins |o| <= 1e6 (their culling ray's range, render_kernels.hip cull_ray).  With
+// filter for ray origins |o| <= 1e6 (their culling ray's range, rt_device.h cull_ray).  With
 // the margin m below (>= 1e6 x that bound) "inside R" (|q - c| <= r_R + EPS) is always true when
 // r_X + m < r_R and always false when r_X - m > r_R + EPS: spinning_globes.scene's glass shells,
 // globes.scene's claw.  A filter whose every literal always passes is skipped (filter_const).
@@ -512,7 +512,7 @@ static void const_filters(FlatScene& f, const RtObject& ob) {
 // surface, any other accepted hit passed R's is_inside test.  R's region is a box in R's own
 // frame (sphere: centre +- (r + EPS), cube: [lo, hi]), so a ray whose image under R's inverse
 // transform misses that box cannot produce an accepted hit of the object.  The kernels test it
-// after the world box (render_kernels.hip obb_may_hit) when its world volume is under half the
+// after the world box (rt_device.h obb_may_hit) when its world volume is under half the
 // world box's -- e.g. globes.scene's tilted axis rod and thin claw slab.
 //
 // Margins (local units, per axis i, on top of the box): the kernel forms o' = xf(inv, o) and
@@ -719,7 +719,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
   f.any_transparent = 0;
   f.shadow_early_out = 1;
   // colour_fast: every operand of every colour op (color.rs:36-90) is finite and >= +0 (no NaN,
-  // no -0, nothing negative), so the kernels' clamps may take the min/max form (render_kernels.hip
+  // no -0, nothing negative), so the kernels' clamps may take the min/max form (rt_device.h
   // in_limit<FC>).  Sufficient: every solid material colour and light colour channel finite with
   // a clear sign bit, every reflectivity and transparency finite, sign bit clear, <= 1.  Then the
   // ambient term, the Lambert intensities (in [0, 1], 0 for NaN angles), the shadow products, the
@@ -736,7 +736,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
   // transparency 1 are skipped).  When every other factor is ONE value T, the product is
   // fl(...fl(fl(1 * T) * T)...) over however many there are -- it depends on the count of T hits and
   // on whether a +-0 hit exists, not on their order -- so the wavefront pair path may evaluate
-  // (shadow ray, object) pairs in any order and fold counts (render_kernels.hip wfp_*).
+  // (shadow ray, object) pairs in any order and fold counts (k_wavefront.hip wfp_*).
   f.shadow_pow = 1;
   f.shadow_t = 0.0;
   bool have_t = false, any_zero = false;

@@ -228,6 +228,11 @@ static int spec_codes(const std::vector<std::string>& srcs, std::vector<std::sha
 }
 
 void spec_program(const FlatScene& f, rt_ctx* c) {
+  // The walks unroll over every hierarchy node and leaf, twice (nearest hit, shadows), and the
+  // shading over every object: code size and compile time grow with the scene (globes.scene, 6
+  // objects and 11 leaves: ~15 k instructions, ~8 s of hipRTC per kernel).  Larger scenes keep the
+  // generic kernels (fractal.scene: 171 objects).
+  c->spec_fits = f.objects.size() <= RT_SPEC_MAX_OBJECTS && f.leaves.size() <= RT_SPEC_MAX_LEAVES;
   c->spec_mode = !f.any_transparent ? RT_MODE_REFL : f.ray_chains ? RT_MODE_CHAIN : RT_MODE_TREE;
   c->spec_fc = f.colour_fast != 0;
   c->spec_deferred = c->spec_mode == RT_MODE_REFL;
@@ -236,7 +241,7 @@ void spec_program(const FlatScene& f, rt_ctx* c) {
 
 int spec_build(rt_ctx* c) {
   spec_drop(c);
-  if (c->spec_src.empty()) return RT_OK;
+  if (c->spec_src.empty() || !c->spec_fits) return RT_OK;   // too large to unroll: the generic kernels
   const std::vector<std::string> srcs = spec_programs(c);
   std::vector<std::shared_ptr<SpecCode>> codes;
   int rc = spec_codes(srcs, &codes, &c->spec_compile_ms);
@@ -267,6 +272,11 @@ extern "C" int rt_scene_precompile(const rt_scene* s, double* compile_ms) {
   rt_ctx tmp;
   tmp.spec_on = 1;
   rt::spec_program(f, &tmp);
+  if (!tmp.spec_fits) {
+    if (compile_ms) *compile_ms = 0.0;
+    return fail(RT_ERR_UNSUPPORTED, "scene of %zu objects / %zu leaves is not specialised (limits %d / %d)",
+                f.objects.size(), f.leaves.size(), RT_SPEC_MAX_OBJECTS, RT_SPEC_MAX_LEAVES);
+  }
   std::vector<std::shared_ptr<SpecCode>> codes;
   double ms = 0.0;
   rc = rt::spec_codes(rt::spec_programs(&tmp), &codes, &ms);

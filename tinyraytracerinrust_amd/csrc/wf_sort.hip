@@ -1,4 +1,4 @@
-// wf_sort.hip -- the wavefront path's per-level ordering (render_kernels.hip "wavefront path"):
+// wf_sort.hip -- the wavefront path's per-level ordering (k_wavefront.hip "wavefront path"):
 // a rocPRIM radix sort (through hipCUB) of (coherence key, slot) pairs.  Own translation unit so the
 // render kernels' file does not compile the library's templates.
 #include <hip/hip_runtime.h>
@@ -18,7 +18,7 @@ extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const u
 // The pair path's sort of (object, pair) by object: few keys (the scene's objects), many items.  A
 // counting sort in three launches (a radix sort of a few million items takes a dozen: rocPRIM's
 // block sort + merge passes below its one-sweep size), not stable -- the pair order within an
-// object does not matter (render_kernels.hip wfp_*: the folds are atomic min / add / or).
+// object does not matter (k_wavefront.hip wfp_*: the folds are atomic min / add / or).
 //   hist:    per workgroup an LDS histogram of its grid-stride share, added to cnt[] (one atomic per
 //            nonzero bin and workgroup);
 //   scan:    one workgroup turns cnt[] into exclusive offsets in place;
