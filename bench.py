@@ -101,6 +101,10 @@ def parse():
                          "alone; 4 at N > 1).  A frame's tail is its costliest tiles, so a lone frame leaves the "
                          "GPU partly idle at its end; overlapping frames fill it (N = 1, --inflight 4: 4K globes "
                          "+2.5 %%, 1080p d5 +37 %%, the sphere +52 %%, profiles/r02bg_inflight_n1.txt)")
+    ap.add_argument("--specialize", type=int, default=1, choices=[0, 1],
+                    help="compile the scene's own row kernels before the timed region (hipRTC, rt_ctx_set_option "
+                         "RT_OPT_SPECIALIZE; the compile time is reported as spec_compile_ms); 0 = the generic kernels. "
+                         "anim120 (120 scenes) always runs the generic kernels")
     ap.add_argument("--chunks", type=int, default=4,
                     help="N > 1, the single-frame phase: the frame as this many sub-frames, each gathered and assembled "
                          "as soon as its bands are rendered, cheapest first (1 = render, then one gather, then assembly)")
@@ -367,6 +371,11 @@ def main():
     # event pair (rt_ctx_last_kernel_ms) is off, as a host that does not read it would run
     # (RT_OPT_TIMING: each timed event costs the stream ~5 us, profiles/r02dc_launch_events.txt)
     rend.set_timing(False)
+    spec_ms = None
+    if a.specialize:
+        t0 = time.perf_counter()
+        rend.set_specialize(1)                            # setup: before the settle / warmup / timed steps
+        spec_ms = round((time.perf_counter() - t0) * 1e3, 1)
 
     layout = a.layout if multi else "contiguous"
     band = a.band if layout == "cyclic" else -(-H // world)
@@ -597,6 +606,8 @@ def main():
         "cpu_baseline": None,
         "frame_check": frame_check,
         "settle": settle,
+        "kernel_code": rend.kernel_info(),
+        "spec_compile_ms": spec_ms,
     }
     if rehearse:
         line.update({"metric": "one-GPU rehearsal of the N-rank pipeline (not a measurement)", "value": None,

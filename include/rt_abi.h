@@ -283,7 +283,7 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  * kernel's ordered launches, RGBA8 / RGB8) take their costliest calibrated tiles out of the main
  * launch and render them in a kernel of their own, started first on an internal stream with a
  * hardware queue of its own, several lanes tracing each pixel's rays together; this many tiles
- * (default 64, at most an eighth of the launch's; 0: none).  Same pixels. */
+ * (default 0 = none; at most an eighth of the launch's).  Same pixels. */
 typedef enum rt_option {
   RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4,
   RT_OPT_WAVEFRONT_PAIRS = 5, RT_OPT_SPECIALIZE = 6, RT_OPT_TAIL_TILES = 7

@@ -38,19 +38,6 @@ render_rows_deferred_kernel(RtDevScene S, int y_first, int band_rows, int band_p
                                     &win);
 }
 
-// The tail kernel (rt_device.h tail_body): the costliest tiles of a tail-bound launch, G lanes per pixel.
-// A few thousand waves at most, whose latency is the point: 2 waves/SIMD, so nothing spills.
-#ifndef RT_WAVES_PER_EU_TAIL
-#define RT_WAVES_PER_EU_TAIL 2
-#endif
-template <bool F64, bool FC, int G>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_TAIL))) void
-render_tail_kernel(RtDevScene S, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth,
-                   uint8_t* __restrict__ out, size_t stride, const int32_t* __restrict__ tiles, int rgb) {
-  __shared__ double s_frames[rows_lds_doubles<RT_MODE_REFL>()];
-  tail_body<F64, FC, G>(S, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, tiles, rgb, (lds_f64*)s_frames);
-}
-
 }  // namespace
 
 using namespace rt;
@@ -230,15 +217,10 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     }
     RT_HIP(hipEventRecord(c->tail_ev0, st));
     RT_HIP(hipStreamWaitEvent(c->tail_stream, c->tail_ev0, 0));
-    const int nl = c->dev.n_leaves;
-    const int G = nl <= 16 ? 16 : nl <= 32 ? 32 : 64;
-    const dim3 tg(slot->n_tail * (unsigned)G);
+    const int rc = launch_tail(c, c->tail_stream, slot->n_tail, a0, a1, a2, a3, max_depth, target, tstride, slot->d_tail,
+                               rgbi, fc);
+    if (rc) return rc;
     hipStream_t ts = c->tail_stream;
-#define RT_LAUNCH_TAIL(FCv, Gv) hipLaunchKernelGGL((render_tail_kernel<false, FCv, Gv>), tg, dim3(64), 0, ts, c->dev, a0, a1, a2, a3, \
-                                                   max_depth, target, tstride, slot->d_tail, rgbi)
-    if (fc) { if (G == 16) RT_LAUNCH_TAIL(true, 16); else if (G == 32) RT_LAUNCH_TAIL(true, 32); else RT_LAUNCH_TAIL(true, 64); }
-    else { if (G == 16) RT_LAUNCH_TAIL(false, 16); else if (G == 32) RT_LAUNCH_TAIL(false, 32); else RT_LAUNCH_TAIL(false, 64); }
-#undef RT_LAUNCH_TAIL
     RT_HIP(hipGetLastError());
     RT_HIP(hipEventRecord(c->tail_ev1, ts));
     c->last_kernel = sfn ? "tail + deferred (specialised)" : "tail + deferred";
@@ -314,7 +296,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
       // the costliest tiles go to the tail kernel (reflection-only scenes, RGBA8 / RGB8 launches): at most
       // an eighth of the launch, never the whole launch
       size_t n_tail = 0;
-      if (!refr && !f64 && c->tail_tiles > 0 && n_tiles >= 16) {
+      if (!refr && !f64 && c->tail_tiles > 0 && n_tiles >= 16 && c->tbl_bytes <= RT_TAIL_MAX_TABLE_BYTES) {
         n_tail = std::min<size_t>((size_t)c->tail_tiles, n_tiles / 8);
         RT_HIP(hipMalloc((void**)&slot->d_tail, n_tail * sizeof(int32_t)));
         RT_HIP(hipMemcpy(slot->d_tail, h_order.data(), n_tail * sizeof(int32_t), hipMemcpyHostToDevice));

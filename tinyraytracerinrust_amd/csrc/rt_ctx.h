@@ -78,7 +78,8 @@ struct rt_ctx {
   uint64_t spec_hash = 0;               // FNV-1a of the program text (the code-object cache key)
   double spec_compile_ms = 0.0;         // 0 when the code object came from the process cache
   const char* last_kernel = "none";     // what the last row launch ran (rt_ctx_kernel_info)
-  int tail_tiles = 64;                  // rt_ctx_set_option(RT_OPT_TAIL_TILES): tiles the tail kernel takes (0: none)
+  int tail_tiles = 0;                   // rt_ctx_set_option(RT_OPT_TAIL_TILES): tiles the tail kernel takes (0: none)
+  size_t tbl_bytes = 0;                 // the blob's tables [objects, texels): what the tail kernel stages in LDS
   hipStream_t tail_stream = nullptr;    // the tail kernel's stream (a hardware queue of its own), made on first use
   hipEvent_t tail_ev0 = nullptr, tail_ev1 = nullptr;
 };
@@ -91,6 +92,7 @@ using rt::fail;
     if (e_ != hipSuccess) return fail(RT_ERR_DEVICE, "%s failed: %s", #call, hipGetErrorString(e_)); \
   } while (0)
 
+#define RT_TAIL_MAX_TABLE_BYTES (48 * 1024)
 #define RT_SPEC_MAX_OBJECTS 32
 #define RT_SPEC_MAX_LEAVES 48
 
@@ -108,6 +110,9 @@ bool diag_env(const char* name);
 // k_wavefront.hip: the wavefront path for rows (y_first, band_rows, band_pitch, n_rows) = a0..a3
 int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int a3, int max_depth, uint8_t* target,
                      size_t tstride, bool f64, int rgbi, size_t n_tiles);
+// k_tail.hip: the tail kernel over n_tail tiles (their indices in d_tail) on stream st
+int launch_tail(rt_ctx* c, hipStream_t st, uint32_t n_tail, int a0, int a1, int a2, int a3, int max_depth,
+                uint8_t* target, size_t tstride, const int32_t* d_tail, int rgbi, bool fc);
 // spec.hip: the specialised program of a flattened scene (at upload), its build (hipRTC, cached per
 // process, module loaded on the context's device) and release
 std::string spec_source(const FlatScene& f, int mode, bool fc, bool deferred);

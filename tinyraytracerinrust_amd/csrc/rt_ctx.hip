@@ -122,6 +122,7 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   d.lights = (const RtLight*)(b + o_lights);
   d.textures = (const RtTexture*)(b + o_tex);
   d.texels = b + o_texels;
+  c->tbl_bytes = o_texels - o_obj;
   d.n_objects = (int32_t)f.objects.size();
   d.n_lights = (int32_t)f.lights.size();
   d.n_leaves = (int32_t)f.leaves.size();

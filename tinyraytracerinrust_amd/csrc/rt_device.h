@@ -116,7 +116,13 @@ namespace {
 
 // Scene tables are read-only for the whole launch: view them through the CONSTANT address space
 // (4) so uniform-index reads compile to scalar (SMEM) loads instead of per-lane VMEM loads.
+// RT_CAS_GENERIC (k_tail.hip): the tables are read through generic (flat) pointers instead -- the tail
+// kernel stages them in LDS, where lanes read different records at LDS latency.
+#ifdef RT_CAS_GENERIC
+#define CAS
+#else
 #define CAS __attribute__((address_space(4)))
+#endif
 template <class T> using cptr = const CAS T*;
 template <class T> __device__ __forceinline__ cptr<T> as_const(const T* p) { return (cptr<T>)p; }
 

@@ -110,14 +110,19 @@ static std::string spec_kernel(int kind, int mode, bool fc, int f64, int cal) {
   static const char* args =
       "(RtDevScene S, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth, uint8_t* __restrict__ out, "
       "size_t stride, const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb)";
-  char buf[1024];
+  char buf[1024], waves[64];
+#ifdef RT_SPEC_WAVES                      // diagnostic builds (make diag): the megakernel's occupancy
+  snprintf(waves, sizeof waves, "%d", RT_SPEC_WAVES);
+#else
+  snprintf(waves, sizeof waves, "RT_WAVES_MODE(%d)", mode);
+#endif
   if (kind == 0)
     snprintf(buf, sizeof buf,
-             "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_MODE(%d)))) "
+             "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(%s))) "
              "void rt_spec_rows_%d%d%s {\n  __shared__ double s_frames[rows_lds_doubles<%d>()];\n"
              "  rows_body<%d, %s, %s, %s>(S, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, order, "
              "cost, rgb, (lds_f64*)s_frames);\n}\n",
-             mode, f64, cal, args, mode, mode, f64 ? "true" : "false", cal ? "true" : "false", fc ? "true" : "false");
+             waves, f64, cal, args, mode, mode, f64 ? "true" : "false", cal ? "true" : "false", fc ? "true" : "false");
   else
     snprintf(buf, sizeof buf,
              "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_DEFERRED))) "

@@ -19,6 +19,20 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _is_render(name, kernel):
+    """The product row kernel of a dispatch: the generic render_rows_kernel<MODE, F64, CAL, FC> with
+    CAL = false, or the scene-specialised rt_spec_rows_<f64><cal> with cal = 0 (the one calibration
+    launch per geometry is excluded)."""
+    if kernel != "render_rows_kernel":
+        return kernel in name
+    m = re.search(r"render_rows_kernel<([^>]*)>", name)
+    if m:
+        a = [x.strip() for x in m.group(1).split(",")]
+        return not (len(a) >= 3 and a[2] == "true")
+    m = re.match(r"rt_spec_rows_(\d)(\d)", name)
+    return bool(m) and m.group(2) == "0"
+
+
 def main(tag="r01", config="globes4k", kernel="render_rows_kernel"):
     out = os.path.join(ROOT, "gpurun_out")
     prof = os.path.join(ROOT, "profiles")
@@ -27,14 +41,12 @@ def main(tag="r01", config="globes4k", kernel="render_rows_kernel"):
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(prof, f"{tag}_kernel_stats.csv"))
     agg = defaultdict(list)
+    names = set()
     for f in glob.glob(os.path.join(out, f"{tag}_pmc_*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            # the product instantiation only: render_rows_kernel<REFR, F64, CAL=false, FC>; the one
-            # calibration launch per geometry (CAL=true, "...ELb1EEEv") is excluded
-            m = re.search(r"render_rows_kernel<([^>]*)>", r["Kernel_Name"])
-            cal = m is not None and len(m.group(1).split(",")) >= 3 and m.group(1).split(",")[2].strip() == "true"
-            if kernel in r["Kernel_Name"] and not cal:
+            if _is_render(r["Kernel_Name"], kernel):
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                names.add(r["Kernel_Name"])
     mean = {k: sum(v) / len(v) for k, v in agg.items()}
     res = {"kernel": kernel, "dispatches_per_counter": {k: len(v) for k, v in agg.items()}, "mean": mean}
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
@@ -48,8 +60,12 @@ def main(tag="r01", config="globes4k", kernel="render_rows_kernel"):
     summ_path = os.path.join(prof, "pmc_summary.json")
     summ = json.load(open(summ_path)) if os.path.exists(summ_path) else {}
     if "hbm_bytes_per_launch" in res:
+        sha_path = os.path.join(out, f"{tag}_so_sha16.txt")
         summ[f"{config}/n1/contiguous"] = {"tag": tag, "hbm_bytes_per_launch": res["hbm_bytes_per_launch"],
-                                           "fetch_kb": mean["FETCH_SIZE"], "write_kb": mean["WRITE_SIZE"]}
+                                           "fetch_kb": mean["FETCH_SIZE"], "write_kb": mean["WRITE_SIZE"],
+                                           "so_sha16": open(sha_path).read().strip() if os.path.exists(sha_path) else None,
+                                           "variant": "spec" if any(n.startswith("rt_spec_") for n in names) else "generic",
+                                           "kernels": sorted(names)}
         if "executed_fp64_flops_per_launch" in res:
             summ[f"{config}/n1/contiguous"]["executed_fp64_flops_per_launch"] = res["executed_fp64_flops_per_launch"]
         if "SQ_INSTS_VALU" in mean and "SQ_WAVES" in mean:
