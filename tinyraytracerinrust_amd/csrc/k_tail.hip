@@ -22,6 +22,9 @@ template <bool FC, int G>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void render_tail_kernel(
     RtDevScene S, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth, uint8_t* __restrict__ out,
     size_t stride, const int32_t* __restrict__ tiles, int rgb, uint32_t tbl_bytes) {
+  // The tail waves share their SIMDs with the main launch's (7 waves/SIMD of the deferred kernel), and
+  // round-robin issue would stretch their latency by as much: they take the highest issue priority.
+  __builtin_amdgcn_s_setprio(3);
   extern __shared__ __attribute__((aligned(16))) uint8_t s_tbl[];   // [frames | tables]
   constexpr uint32_t FRAME_BYTES = rows_lds_doubles<RT_MODE_REFL>() * 8;
   uint8_t* tbl = s_tbl + FRAME_BYTES;

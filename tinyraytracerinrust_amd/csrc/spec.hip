@@ -111,11 +111,14 @@ static std::string spec_kernel(int kind, int mode, bool fc, int f64, int cal) {
       "(RtDevScene S, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth, uint8_t* __restrict__ out, "
       "size_t stride, const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb)";
   char buf[1024], waves[64];
-#ifdef RT_SPEC_WAVES                      // diagnostic builds (make diag): the megakernel's occupancy
-  snprintf(waves, sizeof waves, "%d", RT_SPEC_WAVES);
-#else
-  snprintf(waves, sizeof waves, "RT_WAVES_MODE(%d)", mode);
+  // The specialised megakernel runs 4 waves/SIMD (128 VGPRs): its unrolled walks keep more values
+  // live than the generic loop, and at the generic reflection kernel's 5 waves (96 VGPRs) it spilled
+  // 62 VGPRs; 4 waves measured 4.9 % faster on 4K globes (0.3499 vs 0.3679 ms,
+  // profiles/r05e_spec_waves_ab.txt).  Diagnostic builds may set RT_SPEC_WAVES.
+#ifndef RT_SPEC_WAVES
+#define RT_SPEC_WAVES 4
 #endif
+  snprintf(waves, sizeof waves, "%d", RT_SPEC_WAVES);
   if (kind == 0)
     snprintf(buf, sizeof buf,
              "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(%s))) "

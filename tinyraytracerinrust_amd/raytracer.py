@@ -212,6 +212,7 @@ class Renderer:
         h = ctypes.c_void_p()
         check(lib().rt_ctx_create(int(device), ctypes.byref(h)))
         self.h = h
+        Renderer._register(self)
         self.device = device
         self.width = self.height = 0
 
@@ -374,7 +375,27 @@ class Renderer:
             lib().rt_ctx_free(self.h)
             self.h = ctypes.c_void_p()
 
+    # Contexts still alive at interpreter exit are freed by an atexit hook, registered after torch's
+    # (atexit runs last-registered first) and so while the HIP runtime is still up: a context freed
+    # during module teardown unloaded its specialised modules / freed its buffers after torch had
+    # shut its side of the runtime down (round 4: SIGSEGV / std::bad_variant_access at exit).
+    @classmethod
+    def _register(cls, r: "Renderer") -> None:
+        if "_live" not in cls.__dict__:
+            import atexit
+            import weakref
+            cls._live = weakref.WeakSet()
+            atexit.register(cls.free_all)
+        cls._live.add(r)
+
+    @classmethod
+    def free_all(cls) -> None:
+        for r in list(cls.__dict__.get("_live", ())):
+            r.free()
+
     def __del__(self):
+        if _sys.is_finalizing():
+            return
         try:
             self.free()
         except Exception:
@@ -619,7 +640,7 @@ class HwStream:
 
     @classmethod
     def _register(cls, s: "HwStream") -> None:
-        if not hasattr(cls, "_live"):
+        if "_live" not in cls.__dict__:
             import atexit
             import weakref
             cls._live = weakref.WeakSet()
