@@ -237,7 +237,7 @@ int rt_antialias(rt_ctx* ctx, const uint8_t* src_rgba8, size_t src_stride, doubl
 /* Milliseconds of the last render launch on this context (HIP events recorded on the launch's
  * stream around the kernel; RT_OPT_TIMING 0 turns them off and this call then fails). */
 int rt_ctx_last_kernel_ms(rt_ctx* ctx, float* ms);
-int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launch */
+int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launch (which must still exist) */
 /* Tuning options of a context.  No option changes a single pixel; they only choose how the
  * kernels run.  RT_OPT_KERNEL selects the render kernel for scenes without a transparent object:
  *   RT_KERNEL_AUTO (default): a launch bound by its costliest tiles (fewer tiles than ~5 per wave

@@ -277,7 +277,9 @@ int rt_ctx_synchronize(rt_ctx* c) {
 void rt_ctx_free(rt_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
+  // the whole device, not c->stream: the caller's last stream may be destroyed by now (bench.py's
+  // frames-in-flight streams are; synchronising a destroyed stream crashed at exit in round 4)
+  (void)hipDeviceSynchronize();
   if (c->d_blob) (void)hipFree(c->d_blob);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->wf) (void)hipFree(c->wf);

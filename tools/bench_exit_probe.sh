@@ -1,9 +1,8 @@
 #!/bin/bash
-# Diagnostic: bench.py phases and clean process exit (round 4: aborts / SIGSEGV after the JSON line).
+# Diagnostic: bench.py's default command and clean process exit (round 4: SIGSEGV after the JSON line).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out; mkdir -p $O
-for v in "--no-extra --no-cpu-baseline --specialize 0" "--no-extra --no-cpu-baseline" "--no-cpu-baseline"; do
-  N=$(echo $v | tr -d ' -')
-  timeout -k 5 120 python bench.py --steps 5 --warmup 2 --settle-ms 50 $v > $O/bx_$N.json 2> $O/bx_$N.err
-  echo "[$v] rc=$?"; grep -v amdgpu.ids $O/bx_$N.err | tail -3
+for i in 1 2; do
+  timeout -k 5 180 python -X faulthandler bench.py --steps 20 --warmup 5 > $O/by_$i.json 2> $O/by_$i.err
+  echo "[run $i] rc=$?"; grep -v amdgpu.ids $O/by_$i.err | tail -25
 done
