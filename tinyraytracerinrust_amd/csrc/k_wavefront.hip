@@ -77,9 +77,7 @@ __host__ __device__ __forceinline__ WfLevel wf_level(const WfArena& A, int d) {
 // pixel slot -> (x, output row r); false outside the launch's rows / frame
 __device__ __forceinline__ bool wf_pixel(const RtDevScene& S, uint32_t slot, int y_first, int band_rows, int band_pitch,
                                          int n_rows, int* x, int* r, int* y) {
-  const unsigned tiles_x = (unsigned)(S.width + 7) / 8, tile = slot >> 6, l = slot & 63;
-  *x = (int)(tile % tiles_x) * 8 + (int)(l & 7);
-  *r = (int)(tile / tiles_x) * 8 + (int)(l >> 3);
+  tile_pixel(slot >> 6, (int)(slot & 63), S.width, x, r);
   if (*x >= S.width || *r >= n_rows) return false;
   *y = y_first + (*r / band_rows) * band_pitch + *r % band_rows;
   return *y < S.height;

@@ -34,6 +34,11 @@ using __hip_internal::uint64_t;
 
 // Kernel modes (rt_device.h trace, k_rows.hip): the reflection-only megakernel; refraction scenes
 // whose rays form chains (RtDevScene::ray_chains); refraction scenes with ray trees.
+// Pixel tile of one wave: RT_TILE_W x (64 / RT_TILE_W) pixels (rt_device.h tile_pixel).  8 x 8 by
+// default; diagnostic builds may set 16 (16 x 4) or 32 (32 x 2).
+#ifndef RT_TILE_W
+#define RT_TILE_W 8
+#endif
 #define RT_MODE_REFL 0
 #define RT_MODE_CHAIN 1
 #define RT_MODE_TREE 2

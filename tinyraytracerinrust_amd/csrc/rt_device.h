@@ -1339,7 +1339,14 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
 #define RT_WAVES_MODE(M) ((M) == RT_MODE_REFL ? RT_WAVES_PER_EU_NOREFR : (M) == RT_MODE_CHAIN ? RT_WAVES_PER_EU_CHAIN : RT_WAVES_PER_EU)
 // Workgroup = one wave of 8x8 pixels: measured 3-5 % faster than 2x2-wave workgroups (round 1).
 constexpr int RT_WG_THREADS = 64;
-constexpr int RT_TILE_W = 8, RT_TILE_H = 8;
+// Tile = the 64 pixels of one wave, RT_TILE_W x RT_TILE_H (RT_TILE_W in rt_blob.h).  Pixel `pix` of tile `tile` -> (x, output row r).
+constexpr int RT_TILE_H = 64 / RT_TILE_W;
+static_assert(RT_TILE_W * RT_TILE_H == 64, "a tile is one wave's 64 pixels");
+__device__ __forceinline__ void tile_pixel(unsigned tile, int pix, int width, int* x, int* r) {
+  const unsigned tiles_x = (unsigned)(width + RT_TILE_W - 1) / RT_TILE_W;
+  *x = (int)(tile % tiles_x) * RT_TILE_W + pix % RT_TILE_W;
+  *r = (int)(tile / tiles_x) * RT_TILE_H + pix / RT_TILE_W;
+}
 
 // One pixel's colour into an output row: f64 RGBA (alpha 1 after any colour op), packed RGB8 (band
 // gathers) or RGBA8 with `(c * 255.0) as u8` per channel (easy_pixbuf.rs:46-53).
@@ -1362,22 +1369,21 @@ __device__ __forceinline__ void store_pixel(uint8_t* row, int x, Col c, int rgb)
 // Tile dispatch order (see launch_bands): `order` lists the tiles most expensive first, as measured
 // on a calibration launch that stored each tile's wave time in `cost`.  CAL (the calibration
 // instantiation) is the only one that carries the timing code.
-template <int MODE, bool F64, bool CAL, bool FC>
+// KL_ >= 0: that many stack frames in LDS (the specialised kernels at 4 waves/SIMD have room for more).
+template <int MODE, bool F64, bool CAL, bool FC, int KL_ = -1>
 __device__ __forceinline__ void rows_body(const RtDevScene& S, int y_first, int band_rows, int band_pitch, int n_rows,
                                           int max_depth, uint8_t* __restrict__ out, size_t stride,
                                           const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb,
                                           lds_f64* frames) {
   constexpr bool REFR = MODE != RT_MODE_REFL, CHAIN = MODE == RT_MODE_CHAIN;
   constexpr int KLR = MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0;
-  constexpr int KL = CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES;
+  constexpr int KL = KL_ >= 0 ? KL_ : CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES;
   const int lane = threadIdx.x & 63;
   const unsigned tile = CAL || !order ? blockIdx.x : (unsigned)order[blockIdx.x];
   [[maybe_unused]] uint64_t t_start = 0;
   if constexpr (CAL) t_start = wall_clock64();
-  const unsigned tiles_x = (unsigned)(S.width + RT_TILE_W - 1) / RT_TILE_W;
-  const int bx = (int)(tile % tiles_x), by = (int)(tile / tiles_x);
-  const int x = bx * RT_TILE_W + (lane & 7);
-  const int r = by * RT_TILE_H + (lane >> 3);
+  int x, r;
+  tile_pixel(tile, lane, S.width, &x, &r);
   if (x >= S.width || r >= n_rows) return;
   const int y = y_first + (r / band_rows) * band_pitch + r % band_rows;
   if (y >= S.height) return;
@@ -1388,9 +1394,10 @@ __device__ __forceinline__ void rows_body(const RtDevScene& S, int y_first, int 
   if constexpr (CAL)
     if (threadIdx.x == 0) cost[tile] = (uint32_t)(wall_clock64() - t_start);   // vector store
 }
-template <int MODE>
+template <int MODE, int KL_ = -1>
 constexpr int rows_lds_doubles() {
-  return ((MODE == RT_MODE_CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES) * 4 + (MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0) * 7) * 64;
+  return ((KL_ >= 0 ? KL_ : MODE == RT_MODE_CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES) * 4 +
+          (MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0) * 7) * 64;
 }
 
 // The deferred-shadow kernel's body (reflection-only scenes, or refraction chains on request): one
@@ -1410,9 +1417,8 @@ __device__ __forceinline__ void deferred_body(const RtDevScene& S, int y_first, 
   const int pix = (int)((e >> 20) & 15u) * per + lane;
   [[maybe_unused]] uint64_t t_start = 0;
   if constexpr (CAL) t_start = wall_clock64();
-  const unsigned tiles_x = (unsigned)(S.width + 7) / 8;
-  const int x = (int)(tile % tiles_x) * 8 + (pix & 7);
-  const int r = (int)(tile / tiles_x) * 8 + (pix >> 3);
+  int x, r;
+  tile_pixel(tile, pix, S.width, &x, &r);
   int y = 0;
   bool valid = lane < per && x < S.width && r < n_rows;
   if (valid) {
@@ -1442,9 +1448,8 @@ __device__ __forceinline__ void tail_body(const RtDevScene& S, int y_first, int 
   const int lane = threadIdx.x & 63;
   const unsigned tile = (unsigned)tiles[blockIdx.x / G];
   const int pix = (int)(blockIdx.x % G) * PPW + lane / G;
-  const unsigned tiles_x = (unsigned)(S.width + 7) / 8;
-  const int x = (int)(tile % tiles_x) * 8 + (pix & 7);
-  const int r = (int)(tile / tiles_x) * 8 + (pix >> 3);
+  int x, r;
+  tile_pixel(tile, pix, S.width, &x, &r);
   if (x >= S.width || r >= n_rows) return;                         // the whole group: same pixel
   const int y = y_first + (r / band_rows) * band_pitch + r % band_rows;
   if (y >= S.height) return;

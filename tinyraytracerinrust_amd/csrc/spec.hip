@@ -21,6 +21,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <thread>
 
 #include "rt_ctx.h"
@@ -86,7 +87,8 @@ std::string spec_source(const FlatScene& f, int mode, bool fc, bool deferred) {
   (void)mode; (void)fc; (void)deferred;
   std::string s;
   char buf[256];
-  s += "// scene-specialised row kernels (spec.hip)\n#define RT_SPEC 1\n#include \"rt_blob.h\"\n";
+  s += "// scene-specialised row kernels (spec.hip)\n#define RT_SPEC 1\n#define RT_TILE_W " + std::to_string(RT_TILE_W) +
+       "\n#include \"rt_blob.h\"\n";
   s += "template <int N> struct SpecRaw { unsigned long long w[N]; };\nnamespace rt_spec {\n";
   snprintf(buf, sizeof buf,
            "constexpr int N_OBJECTS = %d, N_LIGHTS = %d, N_TRAV = %d, N_STRAV = %d, SHADOW_EARLY_OUT = %d;\n",
@@ -119,13 +121,20 @@ static std::string spec_kernel(int kind, int mode, bool fc, int f64, int cal) {
 #define RT_SPEC_WAVES 4
 #endif
   snprintf(waves, sizeof waves, "%d", RT_SPEC_WAVES);
+  // stack frames in LDS: 4 waves/SIMD leave 10 KB per one-wave workgroup (the generic kernel's 2
+  // frames at 5 waves: 4 KB); RT_SPEC_LDS_FRAMES (diagnostic builds) overrides the mode's default
+#ifdef RT_SPEC_LDS_FRAMES
+  const int kl = RT_SPEC_LDS_FRAMES;
+#else
+  const int kl = -1;
+#endif
   if (kind == 0)
     snprintf(buf, sizeof buf,
              "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(%s))) "
-             "void rt_spec_rows_%d%d%s {\n  __shared__ double s_frames[rows_lds_doubles<%d>()];\n"
-             "  rows_body<%d, %s, %s, %s>(S, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, order, "
+             "void rt_spec_rows_%d%d%s {\n  __shared__ double s_frames[rows_lds_doubles<%d, %d>()];\n"
+             "  rows_body<%d, %s, %s, %s, %d>(S, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, order, "
              "cost, rgb, (lds_f64*)s_frames);\n}\n",
-             waves, f64, cal, args, mode, mode, f64 ? "true" : "false", cal ? "true" : "false", fc ? "true" : "false");
+             waves, f64, cal, args, mode, kl, mode, f64 ? "true" : "false", cal ? "true" : "false", fc ? "true" : "false", kl);
   else
     snprintf(buf, sizeof buf,
              "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_DEFERRED))) "

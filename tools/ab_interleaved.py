@@ -42,7 +42,9 @@ def main():
     import time
     import torch
     W, H = (int(v) for v in a.size.split("x"))
-    text = open(os.path.join(SCENES, a.scene + ".scene")).read().encode()
+    # "sphere": bench.py's one-line scene of BASELINE config 2
+    text = (b"draw(sphere(<0, 0, 0>, 30, red))" if a.scene == "sphere"
+            else open(os.path.join(SCENES, a.scene + ".scene")).read().encode())
     out = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     ctxs = []
