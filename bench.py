@@ -104,7 +104,8 @@ def parse():
     ap.add_argument("--specialize", type=int, default=1, choices=[0, 1],
                     help="compile the scene's own row kernels before the timed region (hipRTC, rt_ctx_set_option "
                          "RT_OPT_SPECIALIZE; the compile time is reported as spec_compile_ms); 0 = the generic kernels. "
-                         "anim120 (120 scenes) always runs the generic kernels")
+                         "anim120: the frames' scenes registered as scene families (rt_spec_family_register: one "
+                         "program per family of frames of the same structure, compiled before the timed region)")
     ap.add_argument("--chunks", type=int, default=4,
                     help="N > 1, the single-frame phase: the frame as this many sub-frames, each gathered and assembled "
                          "as soon as its bands are rendered, cheapest first (1 = render, then one gather, then assembly)")
@@ -899,16 +900,28 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
     text = open(os.path.join(SCENES, scene + ".scene")).read()
     mine = list(range(rank, F, world))
     t0 = time.perf_counter()
+    scenes = [T.Scene.compile(text, f / F, W, H, asset_dir=SCENES) for f in mine]
+    prep_s = time.perf_counter() - t0
+    spec_ms = None
+    if a.specialize:
+        # setup, as the headline's specialisation: the owned frames' families (one hipRTC program per
+        # family of frames of the same structure; spinning_globes: two), each renderer loads its own
+        t1 = time.perf_counter()
+        T.Scene.register_family(scenes)
+        spec_ms = round((time.perf_counter() - t1) * 1e3, 1)
+    t0 = time.perf_counter()
     rends = []
-    for f in mine:
-        sc = T.Scene.compile(text, f / F, W, H, asset_dir=SCENES)
+    for sc in scenes:
         r = T.Renderer(local)
+        if a.specialize:
+            r.set_specialize(1)
         r.upload(sc)
         r.set_timing(False)                               # bench's own events time the frames
         r.set_kernel(a.kernel)
         rends.append(r)
     torch.cuda.synchronize(dev)
-    prep_ms = (time.perf_counter() - t0) * 1e3 / max(1, len(mine))
+    prep_ms = (prep_s + time.perf_counter() - t0) * 1e3 / max(1, len(mine))
+    variants = sorted({r.kernel_variant() for r in rends})
     outs = [torch.zeros((H, W, 4), dtype=torch.uint8, device=dev) for _ in mine]
     K = max(1, a.streams)
     hw = [] if K == 1 else [T.HwStream(local) for _ in range(K)]      # own hardware queues (main())
@@ -1016,6 +1029,8 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
         }),
         "rays": rays_line(fl, F * W * H * a.steps / elapsed),
         "host_compile_upload_ms_per_frame": round(prep_ms, 3),
+        "kernel_code": "+".join(variants),
+        "spec_compile_ms": spec_ms,
         "settle": settle,
         "cpu_baseline": None,
         "frame_check": frame_check,

@@ -301,6 +301,20 @@ int rt_ctx_kernel_info(rt_ctx* ctx, char* buf, size_t cap);
 int rt_scene_precompile(const rt_scene* scene, double* compile_ms);
 /* The specialised program's text (tests, debugging): cap, len as rt_scene_describe. */
 int rt_scene_spec_program(const rt_scene* scene, char* buf, size_t cap, size_t* len);
+/* Specialised programs for n scenes -- the frames of an animation (the reference's animate mode
+ * builds every frame's scene anew, gui.rs:78-89) -- one per FAMILY of scenes of the same structure:
+ * equal table sizes, object hierarchy, CSG nodes, filter programs, textures and flags; the numbers
+ * may differ.  The words of the flattened tables every member of a family shares are compiled in
+ * as constants, the others are read from the rendering scene's own tables, so a family's one
+ * hipRTC compile serves all its members (the families compile in parallel; *compile_ms = the
+ * longest, 0 if all were cached).  Registered for the process: a context with RT_OPT_SPECIALIZE
+ * whose uploaded scene matches a registered family (a member, or any scene sharing those words)
+ * loads the family's program instead of compiling its own (newest first); set the option after
+ * registering, or upload after it.  RT_ERR_UNSUPPORTED: scenes above the specialisation limits.
+ * Same pixels as the generic kernels. */
+int rt_spec_family_register(const rt_scene* const* scenes, int32_t n, double* compile_ms);
+/* Forget every registered family (contexts keep the programs they loaded). */
+int rt_spec_family_clear(void);
 void rt_ctx_free(rt_ctx* ctx);
 /* A HIP stream on a hardware queue of its own (hipExtStreamCreateWithCUMask with every CU
  * enabled), for renders that overlap: plain streams share the process's few hardware queues

@@ -40,3 +40,26 @@ def test_precompile_without_a_device_and_cache():
     ms = s.precompile()
     assert ms > 0.0
     assert s.precompile() == 0.0                      # the process cache has every program now
+
+
+def test_scene_family_programs():
+    """rt_spec_family_register: the frames of spinning_globes.scene fall into families of the same
+    hierarchy; every member's program is its family's (one text, so one compile), the varying words
+    are masked (VARY_*) and zeroed, the shared ones carried bit for bit; other scenes keep their own."""
+    import tinyraytracerinrust_amd as T
+    text = scene_text("spinning_globes")
+    frames = [_scene(text, f / 12) for f in range(12)]
+    T.Scene.clear_families()
+    try:
+        assert T.Scene.register_family(frames + [_scene(scene_text("globes"))]) >= 0.0
+        progs = [s.spec_program() for s in frames]
+        assert all("#define RT_SPEC_FAMILY 1" in p for p in progs)
+        assert 1 <= len(set(progs)) <= 3, len(set(progs))
+        vary = re.search(r"VARY_OBJECTS\[\] = \{([^}]*)\}", progs[0]).group(1).split(",")
+        assert len(vary) == 4 * 192 // 4 and 0 < vary.count("1") < len(vary)
+        assert "RT_SPEC_FAMILY" in _scene(scene_text("globes")).spec_program()    # a family of one
+        # the exact program of a frame carries its own values where the family's has zeros
+        T.Scene.clear_families()
+        assert "RT_SPEC_FAMILY" not in frames[3].spec_program()
+    finally:
+        T.Scene.clear_families()

@@ -81,6 +81,8 @@ SIGNATURES = {
     "rt_scene_describe": (_I, [_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
     "rt_scene_spec_program": (_I, [_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
     "rt_scene_precompile": (_I, [_P, ctypes.POINTER(ctypes.c_double)]),
+    "rt_spec_family_register": (_I, [ctypes.POINTER(_P), ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]),
+    "rt_spec_family_clear": (_I, []),
     "rt_ctx_kernel_info": (_I, [_P, ctypes.c_char_p, ctypes.c_size_t]),
     "rt_scene_info": (_I, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_U32),

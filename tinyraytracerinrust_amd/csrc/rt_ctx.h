@@ -6,6 +6,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -77,6 +78,9 @@ struct rt_ctx {
   hipFunction_t spec_def[2][2] = {};    // [f64][cal]
   uint64_t spec_hash = 0;               // FNV-1a of the program text (the code-object cache key)
   double spec_compile_ms = 0.0;         // 0 when the code object came from the process cache
+  int spec_family = 0;                  // > 0: the program of a registered scene family of that many members
+  std::shared_ptr<rt::FlatScene> spec_flat;   // the uploaded scene's tables (texels dropped): the program is
+                                        // re-chosen when the option is set (families registered since)
   const char* last_kernel = "none";     // what the last row launch ran (rt_ctx_kernel_info)
   int tail_tiles = 0;                   // rt_ctx_set_option(RT_OPT_TAIL_TILES): tiles the tail kernel takes (0: none)
   size_t tbl_bytes = 0;                 // the blob's tables [objects, texels): what the tail kernel stages in LDS
@@ -115,8 +119,8 @@ int launch_tail(rt_ctx* c, hipStream_t st, uint32_t n_tail, int a0, int a1, int 
                 uint8_t* target, size_t tstride, const int32_t* d_tail, int rgbi, bool fc);
 // spec.hip: the specialised program of a flattened scene (at upload), its build (hipRTC, cached per
 // process, module loaded on the context's device) and release
-std::string spec_source(const FlatScene& f, int mode, bool fc, bool deferred);
 void spec_program(const FlatScene& f, rt_ctx* c);   // the scene's mode, clamp form and program text
 int spec_build(rt_ctx* c);
 void spec_drop(rt_ctx* c);
+const char* spec_compiler();                        // which hipRTC compiles the programs
 }  // namespace rt

@@ -153,7 +153,10 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   // the scene-specialised program (spec.hip): the row kernels of the scene's mode; reflection-only
   // scenes also get the deferred kernels (their tail-bound launches' choice)
   rt::spec_drop(c);
-  rt::spec_program(f, c);
+  c->spec_flat = std::make_shared<rt::FlatScene>(f);
+  c->spec_flat->texels.clear();
+  c->spec_flat->texels.shrink_to_fit();
+  rt::spec_program(*c->spec_flat, c);
   if (c->spec_on) {
     int rc = rt::spec_build(c);
     if (rc) return rc;
@@ -163,11 +166,12 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
 
 int rt_ctx_kernel_info(rt_ctx* c, char* buf, size_t cap) {
   if (!c || !buf || cap == 0) return fail(RT_ERR_INVALID, "null argument");
-  char s[256];
+  char s[640];
   if (c->spec_mod)
-    snprintf(s, sizeof s, "scene-specialised (hipRTC %016llx, %s, compiled in %.0f ms)%s; last launch: %s",
+    snprintf(s, sizeof s, "scene-specialised (hipRTC %016llx, %s%s, compiled in %.0f ms%s by %s); last launch: %s",
              (unsigned long long)c->spec_hash, c->spec_mode == RT_MODE_REFL ? "reflection" : c->spec_mode == RT_MODE_CHAIN ? "chain" : "tree",
-             c->spec_compile_ms, c->spec_compile_ms == 0.0 ? " [process cache]" : "", c->last_kernel);
+             c->spec_family ? (", family of " + std::to_string(c->spec_family) + " scenes").c_str() : "",
+             c->spec_compile_ms, c->spec_compile_ms == 0.0 ? " [process cache]" : "", rt::spec_compiler(), c->last_kernel);
   else if (c->spec_on && c->uploaded && !c->spec_fits)
     snprintf(s, sizeof s, "generic (librt_mi355x.so; scene too large to specialise: > %d objects or > %d leaves); last "
              "launch: %s", RT_SPEC_MAX_OBJECTS, RT_SPEC_MAX_LEAVES, c->last_kernel);
@@ -209,7 +213,9 @@ int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
     RT_HIP(hipDeviceSynchronize());             // launches in flight may still run the modules
     rt::spec_drop(c);
     c->spec_on = value;
-    return c->uploaded && value ? rt::spec_build(c) : RT_OK;
+    if (!c->uploaded || !value) return RT_OK;
+    rt::spec_program(*c->spec_flat, c);         // a scene family registered since the upload may hold it
+    return rt::spec_build(c);
   }
   if (option == RT_OPT_WAVEFRONT_PAIRS) {
     if (value < 0 || value > 2) return fail(RT_ERR_INVALID, "RT_OPT_WAVEFRONT_PAIRS %d not in [0, 2]", value);

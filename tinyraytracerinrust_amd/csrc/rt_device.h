@@ -118,13 +118,39 @@ namespace {
 // (4) so uniform-index reads compile to scalar (SMEM) loads instead of per-lane VMEM loads.
 // RT_CAS_GENERIC (k_tail.hip): the tables are read through generic (flat) pointers instead -- the tail
 // kernel stages them in LDS, where lanes read different records at LDS latency.
-#ifdef RT_CAS_GENERIC
+#if defined(RT_CAS_GENERIC) || defined(RT_SPEC_FAMILY)
 #define CAS
 #else
 #define CAS __attribute__((address_space(4)))
 #endif
 template <class T> using cptr = const CAS T*;
 template <class T> __device__ __forceinline__ cptr<T> as_const(const T* p) { return (cptr<T>)p; }
+
+// Record I of scene table `tab` (objects, trav, strav, leaves, lights) as `cptr<T> NAME`.
+// RT_SPEC_FAMILY (spec.hip: ONE program for a family of scenes of the same structure -- the frames of
+// an animation): the record is assembled word by word, the 4-byte words every member of the family
+// shares from the program's constexpr table (they fold like the single-scene program's), the words
+// that differ between members from this scene's table in HBM (scalar loads).  The table stays
+// exactly the scene's own: the merge only decides which words the compiler may treat as constants.
+#ifdef RT_SPEC_FAMILY
+template <class T> struct FamRec { T v; };
+template <class T, int N>
+__device__ __forceinline__ FamRec<T> fam_rec(const T (&ct)[N], const uint8_t* vary, const T* rt, int i) {
+  constexpr int NW = (int)(sizeof(T) / 4);
+  const uint32_t* cw = (const uint32_t*)(const void*)&ct[i];
+  const __attribute__((address_space(4))) uint32_t* rw =
+      (const __attribute__((address_space(4))) uint32_t*)(const void*)rt + (size_t)i * NW;
+  uint32_t w[NW];
+#pragma unroll
+  for (int k = 0; k < NW; ++k) w[k] = vary[i * NW + k] ? rw[k] : cw[k];
+  return FamRec<T>{__builtin_bit_cast(T, w)};
+}
+#define RT_REC(NAME, S, tab, TAB, I)                                                   \
+  const auto NAME##_rec = fam_rec(rt_spec::TAB, rt_spec::VARY_##TAB, (S).tab, (I)); \
+  const auto NAME = &NAME##_rec.v
+#else
+#define RT_REC(NAME, S, tab, TAB, I) const auto NAME = &(S).tab[I]
+#endif
 
 struct DS {                         // device view of RtDevScene
   cptr<RtObject> objects;
@@ -408,7 +434,8 @@ RT_FN bool leaf_filter(const DS& S, cptr<RtLeaf> L, V3 p) {
     RT_SPEC_UNROLL
     for (int k = 0; k < nl; ++k) {
       const int v = L->lit[k];
-      if (leaf_inside(&S.leaves[v >> 1], p, fin) != (bool)(v & 1)) return false;
+      RT_REC(LI, S, leaves, LEAVES, v >> 1);
+      if (leaf_inside(LI, p, fin) != (bool)(v & 1)) return false;
     }
     return true;
   }
@@ -418,7 +445,8 @@ RT_FN bool leaf_filter(const DS& S, cptr<RtLeaf> L, V3 p) {
   for (int k = L->prog_begin; k < e; ++k) {
     const int op = S.prog[k].op, arg = S.prog[k].arg;
     if (op == RT_OP_INSIDE) {
-      st = (st << 1) | (leaf_inside(&S.leaves[arg], p, fin) ? 1u : 0u);
+      RT_REC(LI, S, leaves, LEAVES, arg);
+      st = (st << 1) | (leaf_inside(LI, p, fin) ? 1u : 0u);
     } else if (op == RT_OP_REQUIRE) {
       uint32_t v = st & 1u;
       st >>= 1;
@@ -484,7 +512,7 @@ __device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) 
 #define RT_OBB 1
 #endif
 __device__ __forceinline__ bool obb_may_hit(const DS& S, cptr<RtObject> O, V3 ro, V3 rd, double tmax) {
-  cptr<RtLeaf> R = &S.leaves[O->obb_leaf];
+  RT_REC(R, S, leaves, LEAVES, O->obb_leaf);
   const double ad = fmax(fmax(fabs(rd.x), fabs(rd.y)), fabs(rd.z));
   if (!(ad >= 0.25 && ad <= 4.0 && fabs(ro.x) <= 1e6 && fabs(ro.y) <= 1e6 && fabs(ro.z) <= 1e6)) return true;
   const V3 o = xf(R->inv, ro);
@@ -511,17 +539,26 @@ __device__ __forceinline__ void spec_for(F&& f) {
     spec_for<I + 1, END>(f);
   }
 }
+// (RT_SPEC_FAMILY: a node's obj and skip are shared by every member of the family, spec.hip checks)
 template <bool SORD, int I, int END, class G, class O>
-__device__ __forceinline__ void spec_walk(G& group, O& object) {
+__device__ __forceinline__ void spec_walk(const DS& S, G& group, O& object) {
   if constexpr (I < END) {
     constexpr RtTrav T = SORD ? rt_spec::STRAV[I] : rt_spec::TRAV[I];
-    cptr<RtTrav> TP = as_const(SORD ? &rt_spec::STRAV[I] : &rt_spec::TRAV[I]);
-    if constexpr (T.obj < 0) {
-      if (group(TP)) spec_walk<SORD, I + 1, T.skip>(group, object);
-      spec_walk<SORD, T.skip, END>(group, object);
+    auto body = [&](cptr<RtTrav> TP) RT_INL {
+      if constexpr (T.obj < 0) {
+        if (group(TP)) spec_walk<SORD, I + 1, T.skip>(S, group, object);
+        spec_walk<SORD, T.skip, END>(S, group, object);
+      } else {
+        object(TP);
+        spec_walk<SORD, I + 1, END>(S, group, object);
+      }
+    };
+    if constexpr (SORD) {
+      RT_REC(TP, S, strav, STRAV, I);
+      body(TP);
     } else {
-      object(TP);
-      spec_walk<SORD, I + 1, END>(group, object);
+      RT_REC(TP, S, trav, TRAV, I);
+      body(TP);
     }
   }
 }
@@ -534,7 +571,7 @@ __device__ __forceinline__ void spec_walk(G& group, O& object) {
 template <bool SORD, bool STOP = false, class G, class O>
 __device__ __forceinline__ void walk_trav(const DS& S, G&& group, O&& object, bool* done = nullptr) {
 #ifdef RT_SPEC
-  spec_walk<SORD, 0, SORD ? rt_spec::N_STRAV : rt_spec::N_TRAV>(group, object);
+  spec_walk<SORD, 0, SORD ? rt_spec::N_STRAV : rt_spec::N_TRAV>(S, group, object);
 #else
   const cptr<RtTrav> TR = SORD ? S.strav : S.trav;
   const int n_tr = SORD ? S.n_strav : S.n_trav;
@@ -580,12 +617,12 @@ RT_FN int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist) {
     if (T->cull == RT_CULL_ALWAYS) return;
     if (T->cull == RT_CULL_BOX && !box_may_hit(T->blo, T->bhi, cr, cull_tmax(best))) return;
     const int o = T->obj;
-    cptr<RtObject> O = &S.objects[o];
+    RT_REC(O, S, objects, OBJECTS, o);
     if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, ro, rd, cull_tmax(best))) return;
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
     RT_SPEC_UNROLL
     for (int l = lb; l < le; ++l) {
-      cptr<RtLeaf> L = &S.leaves[l];
+      RT_REC(L, S, leaves, LEAVES, l);
       if (O->leaf_cull) {
         if (L->cull == RT_CULL_ALWAYS) continue;
         if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, cull_tmax(best))) continue;
@@ -631,13 +668,13 @@ RT_FN double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
     if (done) return;
     if (T->shadow_skip || T->cull == RT_CULL_ALWAYS) return;     // the node's copies (see nearest_hit)
     if (T->cull == RT_CULL_BOX && !box_may_hit(T->blo, T->bhi, cr, tmax)) return;
-    cptr<RtObject> O = &S.objects[T->obj];
+    RT_REC(O, S, objects, OBJECTS, T->obj);
     if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, p, dir, tmax)) return;
     const double tobj = O->transparency;
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
     RT_SPEC_UNROLL
     for (int l = lb; l < le; ++l) {
-      cptr<RtLeaf> L = &S.leaves[l];
+      RT_REC(L, S, leaves, LEAVES, l);
       if (O->leaf_cull) {
         if (L->cull == RT_CULL_ALWAYS) continue;
         if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
@@ -748,7 +785,7 @@ RT_FN void object_normal_uv(const DS& S, cptr<RtObject> O, V3 p, bool want_uv, V
   *u = 0.0;
   *v = 0.0;
   if (cnt == 1) {
-    cptr<RtLeaf> L = &S.leaves[N[0].leaf];
+    RT_REC(L, S, leaves, LEAVES, N[0].leaf);
     *n = leaf_normal(L, p, fin);
     if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
     return;
@@ -759,7 +796,7 @@ RT_FN void object_normal_uv(const DS& S, cptr<RtObject> O, V3 p, bool want_uv, V
     const int nk = N[i].kind, na = N[i].a, nb = N[i].b, nl = N[i].leaf;
     bool bi, bo;
     if (nk < RT_N_UNION) {
-      cptr<RtLeaf> L = &S.leaves[nl];
+      RT_REC(L, S, leaves, LEAVES, nl);
       bi = leaf_inside(L, p, fin);
       bo = leaf_on_surface(L, p, fin);
     } else {
@@ -791,7 +828,7 @@ RT_FN void object_normal_uv(const DS& S, cptr<RtObject> O, V3 p, bool want_uv, V
   RT_SPEC_UNROLL
   for (int l = lb; l < le; ++l) {
     if (!((__ballot(sel == l) >> lane) & 1)) continue;
-    cptr<RtLeaf> L = &S.leaves[l];
+    RT_REC(L, S, leaves, LEAVES, l);
     *n = leaf_normal(L, p, fin);
     if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
   }
@@ -852,7 +889,10 @@ __device__ __forceinline__ void shade_inputs(const DS& S, int oi, V3 p, V3* nrm,
   // every object's inputs are constants: one branch per object, taken by the lanes that hit it
   spec_for<0, rt_spec::N_OBJECTS>([&](auto I) RT_INL {
     constexpr int o = decltype(I)::value;
-    if (oi == o) shade(as_const(&rt_spec::OBJECTS[o]));
+    if (oi == o) {
+      RT_REC(O, S, objects, OBJECTS, o);
+      shade(O);
+    }
   });
 #else
   uint64_t todo = __ballot(oi >= 0);
@@ -1019,7 +1059,7 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
       // operands, so it is formed once and kept for the Lambert term.
 #pragma unroll 1
       for (int k = 0; k < S.n_lights; ++k) {
-        cptr<RtLight> lt = &S.lights[k];
+        RT_REC(lt, S, lights, LIGHTS, k);
         const V3 lv = sub(ld3(lt->p), p);
         double ll, ill;
         len_inv(lv, &ll, &ill);
@@ -1240,7 +1280,7 @@ RT_FN Col trace_deferred(const DS& S, V3 ro, V3 rd, int max_depth, bool valid, S
       for (int k = 0; k < nl; ++k) {                                        // :199-227
         const double tr = win->tr[k * n_pub + base + i];
         if (tr == 0.0) continue;
-        cptr<RtLight> lt = &S.lights[k];
+        RT_REC(lt, S, lights, LIGHTS, k);
         const V3 sdir = normalized(sub(ld3(lt->p), p));
         double ang = rt_acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
         if (ang >= PI_D / 2.0) ang = PI_D - ang;
@@ -1263,19 +1303,29 @@ RT_FN Col trace_deferred(const DS& S, V3 ro, V3 rd, int max_depth, bool valid, S
   return C;
 }
 
-// RT_SPEC: every table is the scene's constexpr copy (k_spec.hip), only the texels stay in HBM.
+// RT_SPEC: every table is the scene's constexpr copy (spec.hip), only the texels stay in HBM;
+// RT_SPEC_FAMILY: the family's constexpr tables plus this scene's own (RT_REC).
 __device__ __forceinline__ DS make_ds(const RtDevScene& s) {
   DS d;
 #ifdef RT_SPEC
+#ifdef RT_SPEC_FAMILY
+  // the merged tables (RT_REC) read this scene's own; nodes, programs and textures are the family's
+  d.objects = as_const(s.objects);
+  d.trav = as_const(s.trav);
+  d.strav = as_const(s.strav);
+  d.leaves = as_const(s.leaves);
+  d.lights = as_const(s.lights);
+#else
   d.objects = as_const(rt_spec::OBJECTS);
   d.trav = as_const(rt_spec::TRAV);
-  d.n_trav = rt_spec::N_TRAV;
   d.strav = as_const(rt_spec::STRAV);
+  d.leaves = as_const(rt_spec::LEAVES);
+  d.lights = as_const(rt_spec::LIGHTS);
+#endif
+  d.n_trav = rt_spec::N_TRAV;
   d.n_strav = rt_spec::N_STRAV;
   d.nodes = as_const(rt_spec::NODES);
-  d.leaves = as_const(rt_spec::LEAVES);
   d.prog = as_const(rt_spec::PROG);
-  d.lights = as_const(rt_spec::LIGHTS);
   d.textures = as_const(rt_spec::TEXTURES);
   d.n_objects = rt_spec::N_OBJECTS;
   d.n_lights = rt_spec::N_LIGHTS;

@@ -12,8 +12,10 @@
 // hipRTC (libhiprtc, ROCm) compiles the program at scene upload; the code object is cached per
 // process by the program text's hash, and loaded as a module on the context's device.  Launches
 // take a specialised kernel when one matches (k_rows.hip), the generic one otherwise.
+#include <dlfcn.h>
 #include <hip/hiprtc.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -31,6 +33,62 @@ namespace {
 // The device headers as text (build/spec_headers.inc: raw string literals made by the Makefile).
 #include "spec_headers.inc"
 
+// The hipRTC the programs compile with: the ROCm installation's own (ROCM_PATH, default /opt/rocm),
+// loaded into a link-map namespace of its own (dlmopen) with the code-object manager (comgr) it
+// loads.  In a process that imported PyTorch first, the plain libhiprtc.so.7 / libamd_comgr.so.3
+// resolve to the copies PyTorch bundles (ROCm 7.0, LLVM 20), whose codegen of the scene-family
+// program came out 3.8x larger (128 VGPRs, 1.4 KB/lane of scratch) and 19x slower than this
+// ROCm's (LLVM 22; profiles/r05v_family_compilers.txt).  If the namespace cannot be made, the
+// process's hipRTC is used and the kernel info says so.
+struct Rtc {
+  hiprtcResult (*create)(hiprtcProgram*, const char*, const char*, int, const char* const*, const char* const*);
+  hiprtcResult (*compile)(hiprtcProgram, int, const char* const*);
+  hiprtcResult (*log_size)(hiprtcProgram, size_t*);
+  hiprtcResult (*log)(hiprtcProgram, char*);
+  hiprtcResult (*code_size)(hiprtcProgram, size_t*);
+  hiprtcResult (*code)(hiprtcProgram, char*);
+  hiprtcResult (*destroy)(hiprtcProgram*);
+  const char* (*err)(hiprtcResult);
+  hiprtcResult (*version)(int*, int*);
+  std::string origin;                  // which hipRTC: the kernel info's "compiler" note
+};
+const Rtc& rtc() {
+  static const Rtc r = [] {
+    Rtc x;
+    const char* root = getenv("ROCM_PATH");
+    const std::string path = std::string(root && *root ? root : "/opt/rocm") + "/lib/libhiprtc.so.7";
+    void* h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    auto sym = [&](const char* n) { return h ? dlsym(h, n) : nullptr; };
+    if (h && sym("hiprtcCreateProgram") && sym("hiprtcCompileProgram") && sym("hiprtcGetCode")) {
+      x.create = (decltype(x.create))sym("hiprtcCreateProgram");
+      x.compile = (decltype(x.compile))sym("hiprtcCompileProgram");
+      x.log_size = (decltype(x.log_size))sym("hiprtcGetProgramLogSize");
+      x.log = (decltype(x.log))sym("hiprtcGetProgramLog");
+      x.code_size = (decltype(x.code_size))sym("hiprtcGetCodeSize");
+      x.code = (decltype(x.code))sym("hiprtcGetCode");
+      x.destroy = (decltype(x.destroy))sym("hiprtcDestroyProgram");
+      x.err = (decltype(x.err))sym("hiprtcGetErrorString");
+      x.version = (decltype(x.version))sym("hiprtcVersion");
+      x.origin = path;
+    } else {
+      x.create = hiprtcCreateProgram;
+      x.compile = hiprtcCompileProgram;
+      x.log_size = hiprtcGetProgramLogSize;
+      x.log = hiprtcGetProgramLog;
+      x.code_size = hiprtcGetCodeSize;
+      x.code = hiprtcGetCode;
+      x.destroy = hiprtcDestroyProgram;
+      x.err = hiprtcGetErrorString;
+      x.version = hiprtcVersion;
+      x.origin = std::string("the process's libhiprtc (") + (h ? "symbols missing" : dlerror()) + ")";
+    }
+    int ma = 0, mi = 0;
+    if (x.version && x.version(&ma, &mi) == HIPRTC_SUCCESS) x.origin += " " + std::to_string(ma) + "." + std::to_string(mi);
+    return x;
+  }();
+  return r;
+}
+
 struct SpecCode {
   std::vector<char> code;              // the linked code object
   double compile_ms = 0.0;
@@ -45,8 +103,11 @@ uint64_t fnv1a(const std::string& s) {
 }
 
 // constexpr T NAME[] = { bit_cast<T>(words), ... }: the host record's exact bits (padding included).
+// vary (a family program): per 4-byte word, 1 = the word differs between the family's members -- it is
+// emitted as 0 and read from the scene's own table (rt_device.h RT_REC), and VARY_NAME lists the mask.
 template <class T>
-void emit_table(std::string& s, const char* type, const char* name, const std::vector<T>& v) {
+void emit_table(std::string& s, const char* type, const char* name, const std::vector<T>& v,
+                const std::vector<uint8_t>* vary = nullptr) {
   static_assert(sizeof(T) % 8 == 0, "spec tables are emitted as 64-bit words");
   constexpr size_t W = sizeof(T) / 8;
   char buf[64];
@@ -60,9 +121,12 @@ void emit_table(std::string& s, const char* type, const char* name, const std::v
     rows.resize(1);
     memset((void*)rows.data(), 0, sizeof(T));
   }
-  for (const T& r : rows) {
+  for (size_t ri = 0; ri < rows.size(); ++ri) {
     uint64_t w[W];
-    memcpy(w, &r, sizeof(T));
+    memcpy(w, &rows[ri], sizeof(T));
+    if (vary && !v.empty())
+      for (size_t i = 0; i < 2 * W; ++i)
+        if ((*vary)[ri * 2 * W + i]) w[i / 2] &= i % 2 ? 0xffffffffull : 0xffffffff00000000ull;
     s += "  __builtin_bit_cast(";
     s += type;
     s += ", SpecRaw<";
@@ -76,31 +140,90 @@ void emit_table(std::string& s, const char* type, const char* name, const std::v
     s += "}}),\n";
   }
   s += "};\n";
+  if (vary) {
+    s += "constexpr uint8_t VARY_";
+    s += name;
+    s += "[] = {";
+    if (v.empty()) s += "0";
+    for (size_t i = 0; i < vary->size(); ++i) s += (*vary)[i] ? (i ? ",1" : "1") : (i ? ",0" : "0");
+    s += "};\n";
+  }
 }
+
+// ---- scene families (rt_spec_family_register): one program for scenes of the same structure
+// The frames of an animation differ in some numbers (an object's centre and transform, a colour)
+// and share everything else -- table sizes, the hierarchy, kinds and flags, most parameters.  A
+// family program holds the words every member shares as constants and reads the others from the
+// rendering scene's own tables (rt_device.h RT_REC), so one hipRTC compile serves every member.
+template <class T>
+void vary_words(const std::vector<T>& a, const std::vector<T>& b, std::vector<uint8_t>* m) {
+  const size_t n = a.size() * sizeof(T) / 4;
+  m->resize(n, 0);
+  const uint32_t* x = (const uint32_t*)(const void*)a.data();
+  const uint32_t* y = (const uint32_t*)(const void*)b.data();
+  for (size_t i = 0; i < n; ++i) (*m)[i] |= x[i] != y[i];
+}
+template <class T>
+bool same_except(const std::vector<T>& a, const std::vector<T>& b, const std::vector<uint8_t>& m) {
+  if (a.size() != b.size()) return false;
+  const uint32_t* x = (const uint32_t*)(const void*)a.data();
+  const uint32_t* y = (const uint32_t*)(const void*)b.data();
+  for (size_t i = 0; i < a.size() * sizeof(T) / 4; ++i)
+    if (!m[i] && x[i] != y[i]) return false;
+  return true;
+}
+template <class T>
+bool same_bytes(const std::vector<T>& a, const std::vector<T>& b) {
+  return a.size() == b.size() && (a.empty() || memcmp(a.data(), b.data(), a.size() * sizeof(T)) == 0);
+}
+
+struct SpecFamily {
+  int members = 0;
+  rt::FlatScene base;                  // member 0, without its texels
+  std::vector<uint8_t> v_obj, v_trav, v_strav, v_leaf, v_light;
+  std::string src;                     // the program's prelude
+};
+std::vector<std::shared_ptr<SpecFamily>> g_families;   // under g_spec_mu; newest last
+
+// Same structure: equal table sizes, flags, hierarchy nodes, CSG nodes, filter programs and
+// texture records (the family program holds those as plain constants).
+bool same_structure(const rt::FlatScene& a, const rt::FlatScene& b) {
+  return a.objects.size() == b.objects.size() && a.trav.size() == b.trav.size() && a.strav.size() == b.strav.size() &&
+         a.leaves.size() == b.leaves.size() && a.lights.size() == b.lights.size() && same_bytes(a.nodes, b.nodes) &&
+         same_bytes(a.prog, b.prog) && same_bytes(a.textures, b.textures) && a.any_transparent == b.any_transparent &&
+         a.shadow_early_out == b.shadow_early_out && a.colour_fast == b.colour_fast && a.ray_chains == b.ray_chains;
+}
+bool family_member(const SpecFamily& F, const rt::FlatScene& f) {
+  return same_structure(F.base, f) && same_except(F.base.objects, f.objects, F.v_obj) &&
+         same_except(F.base.trav, f.trav, F.v_trav) && same_except(F.base.strav, f.strav, F.v_strav) &&
+         same_except(F.base.leaves, f.leaves, F.v_leaf) && same_except(F.base.lights, f.lights, F.v_light);
+}
+
 
 }  // namespace
 
 namespace rt {
 
-// The program's prelude: the scene's tables as constexpr data, then the device code.
-std::string spec_source(const FlatScene& f, int mode, bool fc, bool deferred) {
-  (void)mode; (void)fc; (void)deferred;
+// The program's prelude: the scene's tables as constexpr data, then the device code.  fam: the
+// family's program (the words that differ between members zeroed, their masks emitted).
+static std::string spec_source(const FlatScene& f, const SpecFamily* fam) {
   std::string s;
   char buf[256];
-  s += "// scene-specialised row kernels (spec.hip)\n#define RT_SPEC 1\n#define RT_TILE_W " + std::to_string(RT_TILE_W) +
+  s += std::string("// scene-specialised row kernels (spec.hip)\n#define RT_SPEC 1\n") +
+       (fam ? "#define RT_SPEC_FAMILY 1\n" : "") + "#define RT_TILE_W " + std::to_string(RT_TILE_W) +
        "\n#include \"rt_blob.h\"\n";
   s += "template <int N> struct SpecRaw { unsigned long long w[N]; };\nnamespace rt_spec {\n";
   snprintf(buf, sizeof buf,
            "constexpr int N_OBJECTS = %d, N_LIGHTS = %d, N_TRAV = %d, N_STRAV = %d, SHADOW_EARLY_OUT = %d;\n",
            (int)f.objects.size(), (int)f.lights.size(), (int)f.trav.size(), (int)f.strav.size(), f.shadow_early_out);
   s += buf;
-  emit_table(s, "RtObject", "OBJECTS", f.objects);
-  emit_table(s, "RtTrav", "TRAV", f.trav);
-  emit_table(s, "RtTrav", "STRAV", f.strav);
+  emit_table(s, "RtObject", "OBJECTS", f.objects, fam ? &fam->v_obj : nullptr);
+  emit_table(s, "RtTrav", "TRAV", f.trav, fam ? &fam->v_trav : nullptr);
+  emit_table(s, "RtTrav", "STRAV", f.strav, fam ? &fam->v_strav : nullptr);
   emit_table(s, "RtNode", "NODES", f.nodes);
-  emit_table(s, "RtLeaf", "LEAVES", f.leaves);
+  emit_table(s, "RtLeaf", "LEAVES", f.leaves, fam ? &fam->v_leaf : nullptr);
   emit_table(s, "RtProg", "PROG", f.prog);
-  emit_table(s, "RtLight", "LIGHTS", f.lights);
+  emit_table(s, "RtLight", "LIGHTS", f.lights, fam ? &fam->v_light : nullptr);
   emit_table(s, "RtTexture", "TEXTURES", f.textures);
   s += "}  // namespace rt_spec\n#include \"rt_device.h\"\n";
   return s;
@@ -166,6 +289,8 @@ static std::vector<std::string> spec_programs(const rt_ctx* c) {
   return v;
 }
 
+const char* spec_compiler() { return rtc().origin.c_str(); }
+
 void spec_drop(rt_ctx* c) {
   for (auto& m : c->spec_mods)
     if (m) (void)hipModuleUnload(m);
@@ -181,27 +306,37 @@ static int spec_compile(const std::string& src, SpecCode* out) {
   const char* headers[] = {spec_hdr_rt_device, spec_hdr_rt_blob, spec_hdr_rt_math};
   const char* names[] = {"rt_device.h", "rt_blob.h", "rt_math.h"};
   hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, src.c_str(), "rt_spec.hip", 3, headers, names) != HIPRTC_SUCCESS)
+  const Rtc& R = rtc();
+  if (R.create(&prog, src.c_str(), "rt_spec.hip", 3, headers, names) != HIPRTC_SUCCESS)
     return fail(RT_ERR_DEVICE, "hiprtcCreateProgram failed");
   const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
                         "-mllvm", "-disable-machine-licm"};
   const auto t0 = std::chrono::steady_clock::now();
-  const hiprtcResult r = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+  const hiprtcResult r = R.compile(prog, (int)(sizeof opts / sizeof opts[0]), opts);
   out->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (r != HIPRTC_SUCCESS) {
     size_t n = 0;
-    hiprtcGetProgramLogSize(prog, &n);
+    R.log_size(prog, &n);
     std::string log(n + 1, '\0');
-    hiprtcGetProgramLog(prog, &log[0]);
-    hiprtcDestroyProgram(&prog);
-    return fail(RT_ERR_DEVICE, "hipRTC compile of the specialised kernels failed: %s\n%.2000s", hiprtcGetErrorString(r),
+    R.log(prog, &log[0]);
+    R.destroy(&prog);
+    return fail(RT_ERR_DEVICE, "hipRTC compile of the specialised kernels failed: %s\n%.2000s", R.err(r),
                 log.c_str());
   }
   size_t n = 0;
-  hiprtcGetCodeSize(prog, &n);
+  R.code_size(prog, &n);
   out->code.resize(n);
-  hiprtcGetCode(prog, out->code.data());
-  hiprtcDestroyProgram(&prog);
+  R.code(prog, out->code.data());
+  R.destroy(&prog);
+#ifdef RT_DIAG_ENV
+  if (const char* dir = getenv("RT_SPEC_DUMP_DIR")) {     // diagnostic builds: the code object and its text
+    char path[512];
+    snprintf(path, sizeof path, "%s/spec_%016llx.co", dir, (unsigned long long)fnv1a(src));
+    if (FILE* fo = fopen(path, "wb")) { fwrite(out->code.data(), 1, n, fo); fclose(fo); }
+    snprintf(path, sizeof path, "%s/spec_%016llx.hip", dir, (unsigned long long)fnv1a(src));
+    if (FILE* fo = fopen(path, "wb")) { fwrite(src.data(), 1, src.size(), fo); fclose(fo); }
+  }
+#endif
   return RT_OK;
 }
 
@@ -253,7 +388,17 @@ void spec_program(const FlatScene& f, rt_ctx* c) {
   c->spec_mode = !f.any_transparent ? RT_MODE_REFL : f.ray_chains ? RT_MODE_CHAIN : RT_MODE_TREE;
   c->spec_fc = f.colour_fast != 0;
   c->spec_deferred = c->spec_mode == RT_MODE_REFL;
-  c->spec_src = spec_source(f, c->spec_mode, c->spec_fc, c->spec_deferred);
+  c->spec_family = 0;
+  {                                    // a registered family holding this scene: its program
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    for (auto it = g_families.rbegin(); it != g_families.rend(); ++it)
+      if (family_member(**it, f)) {
+        c->spec_src = (*it)->src;
+        c->spec_family = (*it)->members;
+        return;
+      }
+  }
+  c->spec_src = spec_source(f, nullptr);
 }
 
 int spec_build(rt_ctx* c) {
@@ -318,5 +463,71 @@ extern "C" int rt_scene_spec_program(const rt_scene* s, char* buf, size_t cap, s
     memcpy(buf, text.data(), n);
     buf[n] = 0;
   }
+  return RT_OK;
+}
+
+// rt_spec_family_register (include/rt_abi.h): specialised programs for n scenes (the frames of an
+// animation), one per class of scenes of the same structure and object hierarchy (the frames of
+// spinning_globes.scene fall in two: the hierarchy's grouping follows the globes' positions);
+// contexts whose scene belongs to a class load its program (spec_program).
+static bool same_hierarchy(const std::vector<RtTrav>& a, const std::vector<RtTrav>& b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i)
+    if (a[i].obj != b[i].obj || a[i].skip != b[i].skip) return false;
+  return true;
+}
+extern "C" int rt_spec_family_register(const rt_scene* const* scenes, int32_t n, double* compile_ms) {
+  if (!scenes || n < 1) return fail(RT_ERR_INVALID, "no scenes");
+  std::vector<std::shared_ptr<SpecFamily>> fams;
+  rt::FlatScene f;
+  for (int32_t i = 0; i < n; ++i) {
+    if (!scenes[i]) return fail(RT_ERR_INVALID, "null scene %d", i);
+    int rc = rt::flatten(*scenes[i], &f);
+    if (rc) return rc;
+    f.texels.clear();
+    SpecFamily* F = nullptr;
+    for (auto& x : fams)
+      if (same_structure(x->base, f) && same_hierarchy(x->base.trav, f.trav) && same_hierarchy(x->base.strav, f.strav)) {
+        F = x.get();
+        break;
+      }
+    if (!F) {
+      fams.push_back(std::make_shared<SpecFamily>());
+      F = fams.back().get();
+      F->base = f;
+    }
+    F->members++;
+    vary_words(F->base.objects, f.objects, &F->v_obj);
+    vary_words(F->base.trav, f.trav, &F->v_trav);
+    vary_words(F->base.strav, f.strav, &F->v_strav);
+    vary_words(F->base.leaves, f.leaves, &F->v_leaf);
+    vary_words(F->base.lights, f.lights, &F->v_light);
+  }
+  std::vector<std::string> srcs;
+  for (auto& F : fams) {
+    rt_ctx tmp;
+    tmp.spec_on = 1;
+    rt::spec_program(F->base, &tmp);             // mode / clamp form / size limits of the class
+    if (!tmp.spec_fits)
+      return fail(RT_ERR_UNSUPPORTED, "scenes of %zu objects / %zu leaves are not specialised (limits %d / %d)",
+                  F->base.objects.size(), F->base.leaves.size(), RT_SPEC_MAX_OBJECTS, RT_SPEC_MAX_LEAVES);
+    F->src = rt::spec_source(F->base, F.get());
+    tmp.spec_src = F->src;
+    for (std::string& s : rt::spec_programs(&tmp)) srcs.push_back(std::move(s));
+  }
+  std::vector<std::shared_ptr<SpecCode>> codes;   // every class's programs, compiled in parallel
+  double ms = 0.0;
+  int rc = rt::spec_codes(srcs, &codes, &ms);
+  if (compile_ms) *compile_ms = ms;
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_spec_mu);
+  for (auto& F : fams) g_families.push_back(F);
+  return RT_OK;
+}
+
+// rt_spec_family_clear (include/rt_abi.h): forget every registered family (loaded modules stay)
+extern "C" int rt_spec_family_clear(void) {
+  std::lock_guard<std::mutex> lk(g_spec_mu);
+  g_families.clear();
   return RT_OK;
 }

@@ -182,6 +182,21 @@ class Scene:
         check(lib().rt_scene_precompile(self.h, ctypes.byref(ms)))
         return ms.value
 
+    @staticmethod
+    def register_family(scenes) -> float:
+        """rt_spec_family_register: one specialised program for scenes of the same structure (the
+        frames of an animation); renderers whose scene belongs to it load that program when
+        specialisation is on.  Returns the hipRTC milliseconds (0 when cached)."""
+        arr = (ctypes.c_void_p * len(scenes))(*[s.h.value for s in scenes])
+        ms = ctypes.c_double()
+        check(lib().rt_spec_family_register(arr, len(scenes), ctypes.byref(ms)))
+        return ms.value
+
+    @staticmethod
+    def clear_families() -> None:
+        """rt_spec_family_clear: forget every registered scene family."""
+        check(lib().rt_spec_family_clear())
+
     def camera(self) -> dict:
         out = (ctypes.c_double * 13)()
         check(lib().rt_scene_get_camera(self.h, out))

@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--option", nargs="*", default=[],
                     help="per library (in order): OPT=VAL[,OPT=VAL] context options by number (rt_abi.h rt_option, "
                          "e.g. 6=1 for RT_OPT_SPECIALIZE); '-' for none")
+    ap.add_argument("--family", nargs="*", default=[],
+                    help="per library (in order): F registers the scene's F-frame animation (time f / F) as scene "
+                         "families (rt_spec_family_register) before its options are set; '-' for none")
     a = ap.parse_args()
     import time
     import torch
@@ -63,6 +66,19 @@ def main():
         kern = a.kernel[li] if li < len(a.kernel) and a.kernel[li] != "-" else None
         if kern:
             assert L.rt_ctx_set_option(cx, 0, {"auto": 0, "mega": 1, "deferred": 2}[kern]) == 0
+        fam = int(a.family[li]) if li < len(a.family) and a.family[li] != "-" else 0
+        if fam:
+            L.rt_spec_family_clear()
+            fs = []
+            for f in range(fam):
+                s = ctypes.c_void_p()
+                tf = a.time if fam == 1 else f / fam         # a family of one: the scene itself
+                assert L.rt_scene_compile(text, SCENES.encode(), ctypes.c_double(tf), W, H, ctypes.byref(s)) == 0
+                fs.append(s)
+            arr = (ctypes.c_void_p * fam)(*[s.value for s in fs])
+            ms = ctypes.c_double()
+            assert L.rt_spec_family_register(arr, fam, ctypes.byref(ms)) == 0
+            print(f"{path}: {fam}-frame families registered, {ms.value:.0f} ms", flush=True)
         opt = a.option[li] if li < len(a.option) and a.option[li] != "-" else None
         if opt:
             for kv in opt.split(","):
@@ -71,7 +87,7 @@ def main():
                 rc = L.rt_ctx_set_option(cx, k, v)
                 assert rc == 0, (kv, rc)
                 print(f"{path}: option {k}={v} in {(time.perf_counter() - t0) * 1e3:.0f} ms", flush=True)
-        ctxs.append((path + (f" [{env}]" if env else "") + (f" <{kern}>" if kern else "") + (f" {{{opt}}}" if opt else ""),
+        ctxs.append((path + (f" family{fam}" if fam else "") + (f" [{env}]" if env else "") + (f" <{kern}>" if kern else "") + (f" {{{opt}}}" if opt else ""),
                      L, cx, []))
     for rep in range(a.reps + 3):
         for path, L, cx, ms in ctxs:

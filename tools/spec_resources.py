@@ -4,6 +4,7 @@ compiles them), compiles each with hipcc for gfx950 with the hipRTC options and 
 compiler's resource-usage remarks (VGPRs, spills, scratch bytes per lane, occupancy, LDS).
 
   RT_LIB_PATH=tinyraytracerinrust_amd/build/librt_mi355x_kl4.so python3 tools/spec_resources.py globes 3840 2160 /tmp/spec_res rows_00
+  FAMILY=120 python3 tools/spec_resources.py spinning_globes 1920 1080   (the animation's family program)
 """
 import os
 import re
@@ -25,7 +26,13 @@ def main():
     out = sys.argv[4] if len(sys.argv) > 4 else "/tmp/spec_res"
     only = sys.argv[5] if len(sys.argv) > 5 else None          # regex on the kernel names
     os.makedirs(out, exist_ok=True)
-    text = T.Scene.compile(scene_text(name), 0.0, W, H, asset_dir=SCENES).spec_program()
+    fam = int(os.environ.get("FAMILY", "0"))          # > 0: the program of a FAMILY-frame animation's family
+    if fam:
+        frames = [T.Scene.compile(scene_text(name), f / fam, W, H, asset_dir=SCENES) for f in range(fam)]
+        T.Scene.register_family(frames)
+        text = frames[fam // 2].spec_program()
+    else:
+        text = T.Scene.compile(scene_text(name), 0.0, W, H, asset_dir=SCENES).spec_program()
     cut = text.index('extern "C" __global__')
     prelude, kernels = text[:cut], text[cut:]
     csrc = os.path.join(ROOT, "tinyraytracerinrust_amd", "csrc")
