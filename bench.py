@@ -113,10 +113,12 @@ def parse():
                     help="priority of RCCL's stream (the all-gathers) relative to the render streams")
     ap.add_argument("--pool-streams", action="store_true",
                     help="diagnostic: frames in flight on torch pool streams instead of own-queue streams")
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=2,
                     help="anim120: frames dealt round-robin over this many HIP streams so independent "
                          "frames' kernels overlap (one 1080p frame does not fill the GPU to its end); "
-                         "1 / 2 / 3 / 4 streams: 8226 / 8786 / 8901 / 8913 Mrays/s (profiles/r02cu_anim120_streams.txt)")
+                         "specialised (scene families) 1 / 2 / 4 / 8 streams: 14152 / 14781 / 14452 / 13828 Mrays/s "
+                         "(profiles/r05x_tuning.txt); generic 1 / 2 / 3 / 4: 8226 / 8786 / 8901 / 8913 "
+                         "(profiles/r02cu_anim120_streams.txt)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "mega", "deferred"],
                     help="anim120: the renderers' RT_OPT_KERNEL (auto: the library's choice per launch)")
     ap.add_argument("--settle-ms", type=float, default=300.0,

@@ -8,12 +8,15 @@ import torch
 S = os.path.join(ROOT, "tests", "golden", "scenes")
 W, H, D = 3840, 2160, 10
 text = open(os.path.join(S, "globes.scene")).read().encode()
-for path in sys.argv[1:]:
+SPEC = "--spec" in sys.argv                       # RT_OPT_SPECIALIZE = 1 on every context
+for path in [a for a in sys.argv[1:] if a != "--spec"]:
     L = ctypes.CDLL(os.path.abspath(path))
     sc, cx = ctypes.c_void_p(), ctypes.c_void_p()
     assert L.rt_scene_compile(text, S.encode(), ctypes.c_double(0.0), W, H, ctypes.byref(sc)) == 0
     assert L.rt_ctx_create(0, ctypes.byref(cx)) == 0
     assert L.rt_ctx_upload(cx, sc) == 0
+    if SPEC:
+        assert L.rt_ctx_set_option(cx, 6, 1) == 0
     st = torch.cuda.current_stream().cuda_stream
     for n in (1, 2, 4, 8):
         band = 8
