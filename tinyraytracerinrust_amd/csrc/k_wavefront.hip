@@ -437,15 +437,33 @@ __device__ __forceinline__ bool wf_get_ray(const RtDevScene& S, const WfLevel& l
 // One wave per 64 rays of level d (in key order).  SHADOW = false: every object whose box the ray
 // meets; true: per light, every object whose box the shadow segment meets (objects of transparency 1
 // skipped, as shadow_transparency does).
-// Each lane walks its own path through the hierarchy (per-lane vector loads of one 64-byte RtTrav
-// record per step, which carries the object's box and flags): a wave-uniform walk visits the union
-// of its 64 rays' paths, measured 4-20 % slower here (profiles/r03m_pairs_fractal_timing.txt).
-template <bool SHADOW>
-__global__ __launch_bounds__(64) void wfp_cand_kernel(RtDevScene S, WfArena A, WfPairs P, int d, uint32_t n,
-                                                      int y_first, int band_rows, int band_pitch, int n_rows) {
-  __shared__ uint32_t sk[RT_WFP_BUF], sv[RT_WFP_BUF];
-  const int lane = threadIdx.x & 63;
-  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+// Each lane walks its own path through the hierarchy (one 64-byte RtTrav record per step, which
+// carries the object's box and flags): a wave-uniform walk visits the union of its 64 rays' paths,
+// measured 4-20 % slower here (profiles/r03m_pairs_fractal_timing.txt).
+// A step's record load is the walk's latency: one dependent per-lane load per node, ~100 of them
+// per deep ray on fractal.scene -- the deep levels' dispatches last 45-90 us with a few hundred
+// waves because each wave is that chain (SQ_WAVE_CYCLES counts quad-cycles: the round-3 "8-15 k
+// cycles" per wave are 32-60 k, 15-30 us).  LDS_TRAV: the workgroup (WG_WAVES waves) first copies
+// the hierarchy into LDS and the walks read it there.
+constexpr int RT_WFP_CAND_WAVES = 4;
+constexpr uint32_t RT_WFP_LDS_TRAV_MAX = 640;     // nodes (40 KB) staged at most; larger: global loads
+template <bool SHADOW, bool LDS_TRAV>
+__global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevScene S, WfArena A, WfPairs P, int d,
+                                                                          uint32_t n, int y_first, int band_rows,
+                                                                          int band_pitch, int n_rows) {
+  constexpr int WW = LDS_TRAV ? RT_WFP_CAND_WAVES : 1;
+  __shared__ uint32_t sk_all[WW][RT_WFP_BUF], sv_all[WW][RT_WFP_BUF];
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_trav[];
+  const int lane = threadIdx.x & 63, wv = (int)(threadIdx.x >> 6);
+  uint32_t* sk = sk_all[LDS_TRAV ? wv : 0];
+  uint32_t* sv = sv_all[LDS_TRAV ? wv : 0];
+  const uint32_t i = blockIdx.x * (64u * WW) + threadIdx.x;
+  if constexpr (LDS_TRAV) {                                   // the hierarchy into LDS, once per workgroup
+    const uint4* g = (const uint4*)S.trav;
+    uint4* l = (uint4*)s_trav;
+    for (uint32_t q = threadIdx.x; q < (uint32_t)S.n_trav * (sizeof(RtTrav) / 16); q += blockDim.x) l[q] = g[q];
+    __syncthreads();
+  }
   const WfLevel lv = wf_level(A, d);
   const DS D = make_ds(S);
   bool live = i < n;
@@ -456,14 +474,22 @@ __global__ __launch_bounds__(64) void wfp_cand_kernel(RtDevScene S, WfArena A, W
     if (!SHADOW) live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
   }
   uint32_t nb = 0;                                           // wave-uniform fill of the LDS buffer
+  auto wave_sync = []() {                                    // the wave's own buffer: a wave-level barrier
+    if constexpr (LDS_TRAV) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      __syncthreads();
+    }
+  };
   auto flush = [&]() {
-    __syncthreads();
+    wave_sync();
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(P.count + (SHADOW ? 1 : 0), nb);
     base = (uint32_t)__shfl((int)base, 0);
     for (uint32_t q = (uint32_t)lane; q < nb; q += 64)
       if (base + q < P.cap) { P.key[base + q] = sk[q]; P.val[base + q] = sv[q]; }
-    __syncthreads();
+    wave_sync();
     nb = 0;
   };
   auto emit = [&](bool h, uint32_t ob, uint32_t id) {
@@ -480,7 +506,7 @@ __global__ __launch_bounds__(64) void wfp_cand_kernel(RtDevScene S, WfArena A, W
   };
   auto walk = [&](bool act0, V3 o, V3 dir, double tmax, uint32_t id) {
     const CullRay cr = cull_ray(o, dir);
-    const RtTrav* __restrict__ TR = S.trav;
+    const RtTrav* __restrict__ TR = LDS_TRAV ? (const RtTrav*)(const void*)s_trav : S.trav;
     const int nt = S.n_trav;
     int t = act0 ? 0 : nt;
     while (__ballot(t < nt)) {
@@ -700,9 +726,12 @@ using namespace rt;
 extern "C" hipError_t rt_wf_bucket_sort(const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
                                         uint32_t* vals_out, uint32_t n, const uint32_t* n_dev, uint32_t nb, int shift,
                                         uint32_t* cnt, bool zero_cnt, hipStream_t stream);
+#ifdef RT_WF_RADIX_SORT
 extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                                        const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit,
                                        hipStream_t stream);
+#endif
+#define RT_WF_LEVEL_BINS 4096u          // bucket-sort bins of a non-pair level (the key's top 12 bits)
 
 // Pair-path arrays (above, "wavefront pair path"): per ray of a level (R = the larger of
 // the pixel slots and the level capacity) and, grow-only, the pair lists for `need` pairs.
@@ -772,6 +801,20 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
   const dim3 g((n + 63) / 64), b64(64);
   const uint32_t nobj = (uint32_t)c->dev.n_objects;
   uint32_t* bins[3] = {P.bins, P.bins + 4096, P.bins + 8192};
+  // the candidate walks: hierarchies of up to RT_WFP_LDS_TRAV_MAX nodes staged in LDS (4-wave groups)
+  const bool lds_trav = (uint32_t)c->dev.n_trav <= RT_WFP_LDS_TRAV_MAX && !diag_env("RT_WFP_GLOBAL_TRAV");
+  auto launch_cand = [&](bool shadow) {
+    if (lds_trav) {
+      const dim3 gl((n + 64 * RT_WFP_CAND_WAVES - 1) / (64 * RT_WFP_CAND_WAVES)), bl(64 * RT_WFP_CAND_WAVES);
+      const size_t lds = (size_t)c->dev.n_trav * sizeof(RtTrav);
+      if (shadow) hipLaunchKernelGGL((wfp_cand_kernel<true, true>), gl, bl, lds, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+      else hipLaunchKernelGGL((wfp_cand_kernel<false, true>), gl, bl, lds, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+    } else if (shadow) {
+      hipLaunchKernelGGL((wfp_cand_kernel<true, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+    } else {
+      hipLaunchKernelGGL((wfp_cand_kernel<false, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+    }
+  };
   for (;;) {
     // grid-stride evaluations: one pass covers ~4 pairs per ray of the level (fractal: ~3), capped at
     // 8 waves per SIMD -- small levels then launch hundreds, not thousands, of idle workgroups
@@ -779,7 +822,7 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
                                                                           (uint32_t)c->n_cu * 32u)));
     RT_HIP(hipMemsetAsync(P.count, 0, 8, st));
     RT_HIP(hipMemsetAsync(P.bins, 0, 3 * 16384, st));        // the three sorts' bucket counters
-    hipLaunchKernelGGL((wfp_cand_kernel<false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+    launch_cand(false);
     RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count, nobj, 0, bins[0], false, st));
     hipLaunchKernelGGL(wfp_near_eval_kernel, ge, b64, 0, st, c->dev, A, P, d, a0, a1, a2, a3);
     hipLaunchKernelGGL(wfp_near_tie_kernel, dim3(std::min<uint32_t>((P.cap + 255) / 256, 4096)), dim3(256), 0, st, P);
@@ -791,7 +834,7 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
     hipLaunchKernelGGL(wfp_hit_key_kernel, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, c->dev,
                        A, P, d, n, a0, a1, a2, a3, cbits);
     RT_HIP(rt_wf_bucket_sort(P.hkey, P.hkey_s, P.hval, P.hperm, n, nullptr, (nobj + 1u) << cbits, 0, bins[1], false, st));
-    hipLaunchKernelGGL((wfp_cand_kernel<true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+    launch_cand(true);
     RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count + 1, nobj, 0, bins[2], false, st));
     hipLaunchKernelGGL(wfp_shadow_eval_kernel, ge, b64, 0, st, c->dev, P);
     if (refr && fc) hipLaunchKernelGGL((wfp_shade_kernel<true, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
@@ -821,8 +864,15 @@ int rt::launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int 
                             size_t tstride, bool f64, int rgbi, size_t n_tiles) {
   const size_t slots = n_tiles * 64, cap = std::max<size_t>(64, (slots * (size_t)c->wf_cap_pct / 100 + 63) & ~(size_t)63);
   if (cap > 0x7fffffffull || slots > 0x7fffffffull) return fail(RT_ERR_UNSUPPORTED, "wavefront launch of %zu pixel slots too large", slots);
+  // the non-pair levels' coherence order: the in-tree bucket sort on the key's top 12 bits (direction
+  // octant + the 8^3-cell Morton prefix); only the processing order depends on it, never a value
+  // (diagnostic builds with RT_WF_RADIX_SORT: the full 30-bit rocPRIM radix sort it replaced)
+#ifdef RT_WF_RADIX_SORT
   size_t sort_bytes = 0;
   RT_HIP(rt_wf_sort_pairs(nullptr, &sort_bytes, nullptr, nullptr, nullptr, nullptr, (int)cap, 30, st));
+#else
+  const size_t sort_bytes = RT_WF_LEVEL_BINS * 4;
+#endif
   const size_t levels = slots * RT_WF_BYTES0 + (size_t)max_depth * cap * RT_WF_BYTES;
   const size_t o_cnt = (levels + 255) & ~(size_t)255, o_ovf = o_cnt + 256, o_kout = (o_ovf + slots + 255) & ~(size_t)255;
   const size_t o_perm = o_kout + cap * 4, o_tmp = (o_perm + cap * 4 + 255) & ~(size_t)255, bytes = o_tmp + sort_bytes + 256;
@@ -867,8 +917,12 @@ int rt::launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int 
       // evaluations run in object order, and the sort measured 0.3-0.6 ms per fractal frame slower
       // than none (profiles/r03o_sort_ab.txt).
       if (!pairs_level(d)) {
+#ifdef RT_WF_RADIX_SORT
         size_t tb = sort_bytes;
         RT_HIP(rt_wf_sort_pairs(tmp, &tb, L.key, kout, L.val, perm, (int)n, 30, st));
+#else
+        RT_HIP(rt_wf_bucket_sort(L.key, kout, L.val, perm, n, nullptr, RT_WF_LEVEL_BINS, 30 - 12, (uint32_t*)tmp, true, st));
+#endif
         A.perm = perm;
       }
     }

@@ -1,11 +1,15 @@
-// wf_sort.hip -- the wavefront path's per-level ordering (k_wavefront.hip "wavefront path"):
-// a rocPRIM radix sort (through hipCUB) of (coherence key, slot) pairs.  Own translation unit so the
-// render kernels' file does not compile the library's templates.
+// wf_sort.hip -- the wavefront path's orderings (k_wavefront.hip): the in-tree bucket sort below
+// orders the pair path's (object, pair) lists, its hit points, and the non-pair levels' rays by the
+// top 12 bits of their coherence key.  (Diagnostic builds with RT_WF_RADIX_SORT keep the rocPRIM radix
+// sort through hipCUB the non-pair levels used before round 4, for A/B runs.)
 #include <hip/hip_runtime.h>
+#ifdef RT_WF_RADIX_SORT
 #include <hipcub/hipcub.hpp>
+#endif
 #include <stdint.h>
 #include <algorithm>
 
+#ifdef RT_WF_RADIX_SORT
 // d_temp == nullptr: *temp_bytes = the scratch the sort of n pairs needs.  Sorts bits [0, end_bit).
 extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                                        const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit,
@@ -13,6 +17,7 @@ extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const u
   return hipcub::DeviceRadixSort::SortPairs(d_temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out, n, 0, end_bit,
                                             stream);
 }
+#endif
 
 // ---------------------------------------------------------------------------- bucket sort
 // The pair path's sort of (object, pair) by object: few keys (the scene's objects), many items.  A
@@ -21,7 +26,9 @@ extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const u
 // object does not matter (k_wavefront.hip wfp_*: the folds are atomic min / add / or).
 //   hist:    per workgroup an LDS histogram of its grid-stride share, added to cnt[] (one atomic per
 //            nonzero bin and workgroup);
-//   scan:    one workgroup turns cnt[] into exclusive offsets in place;
+//   scan:    one workgroup turns cnt[] into exclusive offsets in place (a launch of its own: fusing it
+//            into hist's last workgroup needs a device-scope fence per workgroup, which writes back
+//            the L2s of the 8 XCDs -- measured 3.6x slower hist, profiles/r05z_wavefront_round4.txt);
 //   scatter: per workgroup a contiguous chunk: LDS counts give each item its rank among the chunk's
 //            items of its key, one atomic per nonzero bin reserves the chunk's run in that bucket.
 #define RT_BS_MAX_BINS 4096
