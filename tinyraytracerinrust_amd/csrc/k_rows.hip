@@ -251,8 +251,13 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     RT_HIP(hipEventRecord(c->tev1, st));
     RT_HIP(hipEventSynchronize(c->tev1));
     RT_HIP(hipEventElapsedTime(&mega_ms, c->tev0, c->tev1));
-    RT_HIP(hipEventRecord(c->tev0, st));
+    // one untimed wavefront launch first: it allocates (or grows) the wavefront and pair arenas, which
+    // the megakernel's timed launch had no counterpart of (a cold first launch could otherwise decide
+    // the choice for the geometry)
     int rc = launch_wavefront(c, st, a0, a1, a2, a3, max_depth, target, tstride, f64, rgbi, n_tiles);
+    if (rc) return rc;
+    RT_HIP(hipEventRecord(c->tev0, st));
+    rc = launch_wavefront(c, st, a0, a1, a2, a3, max_depth, target, tstride, f64, rgbi, n_tiles);
     if (rc) return rc;
     RT_HIP(hipEventRecord(c->tev1, st));
     RT_HIP(hipEventSynchronize(c->tev1));

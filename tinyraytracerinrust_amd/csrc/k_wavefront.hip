@@ -350,7 +350,7 @@ struct WfPairs {
   uint32_t *key_s, *val_s;      // sorted by object
   double* tp;                   // nearest pass: the sorted pair's object's nearest accepted distance
   uint32_t* count;              // [0] / [1]: pairs the nearest / shadow pass emitted (may exceed cap: the host
-                                //   grows the arena and runs the level again)
+                                //   grows the arena and runs the level again); [2]: a count passed 2^31
   uint32_t* bins;               // bucket-sort scratch (RT_BS_MAX_BINS words)
   uint32_t cap;
   unsigned long long* tmin;     // per ray of the level: nearest accepted distance (bits; +inf: none)
@@ -365,6 +365,7 @@ struct WfPairs {
 constexpr unsigned long long RT_WFP_NONE = 0x7FF0000000000000ull;   // +inf
 constexpr int RT_WFP_COUNT = 32;      // the pair counts' words in WfArena::count (after the level counts)
 static_assert(RT_MAX_DEPTH_CAP + 3 <= RT_WFP_COUNT, "wavefront counter block");
+static_assert(RT_WFP_COUNT + 3 <= 64, "wavefront counter block: 256 bytes");
 
 // The object's nearest accepted distance for one ray: nearest_hit's body for one object, its best
 // starting at +inf (the leaf boxes' tmax only shrinks, as share_prev requires).
@@ -485,7 +486,12 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
   auto flush = [&]() {
     wave_sync();
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(P.count + (SHADOW ? 1 : 0), nb);
+    if (lane == 0) {
+      base = atomicAdd(P.count + (SHADOW ? 1 : 0), nb);
+      // a 32-bit count past 2^31 (the arena's limit) is about to wrap: flag the level as failed (the
+      // writes below stay inside the arena; the host reports the overflow instead of using the pairs)
+      if (base >= 0x80000000u) atomicOr(P.count + 2, 1u);
+    }
     base = (uint32_t)__shfl((int)base, 0);
     for (uint32_t q = (uint32_t)lane; q < nb; q += 64)
       if (base + q < P.cap) { P.key[base + q] = sk[q]; P.val[base + q] = sv[q]; }
@@ -820,7 +826,7 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
     // 8 waves per SIMD -- small levels then launch hundreds, not thousands, of idle workgroups
     const dim3 ge(std::max<uint32_t>((uint32_t)c->n_cu, std::min<uint32_t>((uint32_t)(((size_t)n * 4 + 63) / 64),
                                                                           (uint32_t)c->n_cu * 32u)));
-    RT_HIP(hipMemsetAsync(P.count, 0, 8, st));
+    RT_HIP(hipMemsetAsync(P.count, 0, 12, st));
     RT_HIP(hipMemsetAsync(P.bins, 0, 3 * 16384, st));        // the three sorts' bucket counters
     launch_cand(false);
     RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count, nobj, 0, bins[0], false, st));
@@ -842,9 +848,10 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
     else if (fc) hipLaunchKernelGGL((wfp_shade_kernel<false, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
     else hipLaunchKernelGGL((wfp_shade_kernel<false, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
     RT_HIP(hipGetLastError());
-    uint32_t cb[RT_WFP_COUNT + 2];        // the whole counter block in one copy: level counts, pair counts
+    uint32_t cb[RT_WFP_COUNT + 3];        // the whole counter block in one copy: level counts, pair counts, wrap flag
     RT_HIP(hipMemcpyAsync(cb, A.count, sizeof cb, hipMemcpyDeviceToHost, st));
     RT_HIP(hipStreamSynchronize(st));
+    if (cb[RT_WFP_COUNT + 2]) return fail(RT_ERR_UNSUPPORTED, "wavefront pair count of level %d passed 2^31", d);
     *next = d < max_depth ? cb[d + 1] : 0u;
     const uint32_t pc[2] = {cb[RT_WFP_COUNT], cb[RT_WFP_COUNT + 1]};
     if (pc[0] <= P.cap && pc[1] <= P.cap) return RT_OK;
@@ -901,7 +908,10 @@ int rt::launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int 
   RT_HIP(hipMemsetAsync(A.count, 0, 256, st));
   RT_HIP(hipMemsetAsync(A.ovf, 0, slots, st));
   const bool refr = c->dev.any_transparent != 0, fc = c->dev.colour_fast != 0 && c->fast_clamp;
-  const bool pairs = c->wf_pairs > 0 && c->dev.shadow_pow != 0 && c->dev.n_objects > 0 && c->dev.n_objects < 4096;
+  // the pair path's shadow-ray ids (slot * n_lights + light) are 32-bit: launches whose ids would not
+  // fit keep the wave walk (its counts are checked against 2^31 on the device, wfp_cand_kernel)
+  const bool pairs = c->wf_pairs > 0 && c->dev.shadow_pow != 0 && c->dev.n_objects > 0 && c->dev.n_objects < 4096 &&
+                     (uint64_t)std::max(slots, cap) * (uint64_t)std::max(1, c->dev.n_lights) < (1ull << 32);
   auto pairs_level = [&](int d) { return pairs && (d > 0 || c->wf_pairs == 2); };
   uint32_t n_level[RT_MAX_DEPTH_CAP + 2] = {0};
   n_level[0] = (uint32_t)slots;
