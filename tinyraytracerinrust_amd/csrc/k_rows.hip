@@ -281,7 +281,13 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     bool tail_bound = false;
     // wave slots of the calibrated (mega)kernel on this device
     const double slots = (double)c->n_cu * 4.0 * (double)(!refr ? RT_WAVES_PER_EU_NOREFR : c->dev.ray_chains ? RT_WAVES_PER_EU_CHAIN : RT_WAVES_PER_EU);
-    if (auto_ok && dmode == -1 && n_tiles < RT_DEFERRED_MAX_TILES) {
+    // With the scene-specialised megakernel loaded for these launches its costliest tiles finish so
+    // much sooner that the deferred kernel no longer pays anywhere: lone 4K rank shares at N = 4 / 8
+    // (tail ratios 1.6 / 3.0) 0.109 / 0.098 ms against 0.156 / 0.117 ms deferred, 1080p d5 (ratio 1.6)
+    // 0.104 against 0.136 ms (profiles/r06d_kernel_choice.txt): the tail-bound choice is for the
+    // generic kernels only.
+    const bool spec_mega = c->spec_mod && c->spec_mode == RT_MODE_REFL && c->spec_rows[f64 ? 1 : 0][0] && fc == c->spec_fc;
+    if (auto_ok && dmode == -1 && n_tiles < RT_DEFERRED_MAX_TILES && !spec_mega) {
       uint64_t sum = 0, mx = 0;
       for (uint32_t v : h_cost) { sum += v; mx = v > mx ? v : mx; }
       tail_bound = (double)mx > (double)sum / slots;
