@@ -48,7 +48,7 @@ def test_globes4k_specialised_full_frame(worldmap):
 @pytest.mark.parametrize("world", [8, 4])
 def test_globes4k_rank_bands_specialised(worldmap, world):
     """A rank's share of the 4K frame at N = 8 / 4: the ordered launches take the specialised
-    deferred-shadow kernel with split costly tiles (N = 8) or the specialised megakernel (N = 4)."""
+    megakernel (the library's choice once it is loaded, k_rows.hip launch_bands)."""
     import torch
     from tinyraytracerinrust_amd import distributed as D
     W, H = 3840, 2160
