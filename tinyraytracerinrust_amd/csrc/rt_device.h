@@ -1400,6 +1400,20 @@ __device__ __forceinline__ void tile_pixel(unsigned tile, int pix, int width, in
 
 // One pixel's colour into an output row: f64 RGBA (alpha 1 after any colour op), packed RGB8 (band
 // gathers) or RGBA8 with `(c * 255.0) as u8` per channel (easy_pixbuf.rs:46-53).
+// The RGBA8 / RGB8 frame is written once and read by another kernel or the host: nontemporal
+// (streaming) stores.  A wave's 8x8 tile covers a quarter of eight 128-byte lines and the tiles
+// sharing a line run at different times on different XCDs, so through the L2s every row segment
+// reached memory as its own partial-line write-back: WRITE_SIZE counted 118 MiB for a 31.6 MiB
+// background-only 4K frame, 71 MiB with streaming stores, at equal kernel time
+// (profiles/r06h_nt_stores.txt).  Diagnostic builds with RT_PLAIN_STORES keep plain stores.
+template <class T>
+__device__ __forceinline__ void frame_store(T v, T* p) {
+#ifdef RT_PLAIN_STORES
+  *p = v;
+#else
+  __builtin_nontemporal_store(v, p);
+#endif
+}
 template <bool F64>
 __device__ __forceinline__ void store_pixel(uint8_t* row, int x, Col c, int rgb) {
   if constexpr (F64) {
@@ -1407,9 +1421,11 @@ __device__ __forceinline__ void store_pixel(uint8_t* row, int x, Col c, int rgb)
     o[0] = c.r; o[1] = c.g; o[2] = c.b; o[3] = 1.0;
   } else if (rgb) {
     uint8_t* o = row + (size_t)x * 3;
-    o[0] = (uint8_t)to_u8(c.r); o[1] = (uint8_t)to_u8(c.g); o[2] = (uint8_t)to_u8(c.b);
+    frame_store((uint8_t)to_u8(c.r), o);
+    frame_store((uint8_t)to_u8(c.g), o + 1);
+    frame_store((uint8_t)to_u8(c.b), o + 2);
   } else {
-    ((uint32_t*)row)[x] = to_u8(c.r) | (to_u8(c.g) << 8) | (to_u8(c.b) << 16) | (255u << 24);
+    frame_store(to_u8(c.r) | (to_u8(c.g) << 8) | (to_u8(c.b) << 16) | (255u << 24), (uint32_t*)row + x);
   }
 }
 
