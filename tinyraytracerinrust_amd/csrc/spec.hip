@@ -312,7 +312,20 @@ static int spec_compile(const std::string& src, SpecCode* out) {
   const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
                         "-mllvm", "-disable-machine-licm"};
   const auto t0 = std::chrono::steady_clock::now();
+#ifdef RT_DIAG_ENV
+  // diagnostic builds: RT_SPEC_OPTS appends options (space-separated) for compiler A/B runs
+  std::vector<std::string> extra;
+  std::vector<const char*> all(opts, opts + sizeof opts / sizeof opts[0]);
+  if (const char* e = getenv("RT_SPEC_OPTS")) {
+    std::string s(e), w;
+    for (size_t i = 0; i <= s.size(); ++i)
+      if (i == s.size() || s[i] == ' ') { if (!w.empty()) extra.push_back(w); w.clear(); } else w += s[i];
+  }
+  for (const std::string& x : extra) all.push_back(x.c_str());
+  const hiprtcResult r = R.compile(prog, (int)all.size(), all.data());
+#else
   const hiprtcResult r = R.compile(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+#endif
   out->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (r != HIPRTC_SUCCESS) {
     size_t n = 0;
