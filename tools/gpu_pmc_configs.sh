@@ -1,0 +1,18 @@
+#!/bin/bash
+# PMC passes (HBM traffic, executed FP64, issue counters) of the globes1080d5 and sphere1080d0 bench
+# configs at HEAD, for tools/pmc_summary.py (their bench lines' roofline blocks read them).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out
+T=${TAG:-r06l}
+for C in globes1080d5 sphere1080d0; do
+  sha256sum tinyraytracerinrust_amd/librt_mi355x.so | cut -c1-16 > $O/${T}_${C}_so_sha16.txt
+  for PMC in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64" "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES" "SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT"; do
+    N=$(echo $PMC | tr ' ' '_' | cut -c1-40)
+    timeout -s KILL 150 rocprofv3 --pmc $PMC --output-format csv -d $O/${T}_${C}_pmc_$N -o run -- python3 bench.py --config $C --steps 5 --warmup 1 --no-cpu-baseline --no-extra > /dev/null 2> $O/${T}_${C}_pmc_$N.err || { echo "pmc $C $PMC failed"; tail $O/${T}_${C}_pmc_$N.err; exit 1; }
+  done
+done
+timeout -k 10 300 python bench.py --config globes1080d5 --steps 20 --warmup 2 > $O/${T}_bench_globes1080d5.json 2> $O/${T}_b1.err || exit 1
+timeout -k 10 300 python bench.py --config sphere1080d0 --steps 20 --warmup 2 > $O/${T}_bench_sphere1080d0.json 2> $O/${T}_b2.err || exit 1
+echo done
