@@ -369,16 +369,30 @@ def main():
     scene = scene or "sphere"
     rt = T.RayTracer(W, H, device=local)
     rt.load_scene(text, t, asset_dir=SCENES)
-    rend = rt.renderer                                    # uploads the scene blob + texture
+    t_up = time.perf_counter()
+    # the upload: the scene blob + texture to HBM, and (the library's default, RT_OPT_SPECIALIZE 1) the
+    # request for the scene's specialised program, compiled by the library's pool in the background
+    rend = rt.renderer
     # bench times the launches with its own events on the launch stream: the library's per-launch
     # event pair (rt_ctx_last_kernel_ms) is off, as a host that does not read it would run
     # (RT_OPT_TIMING: each timed event costs the stream ~5 us, profiles/r02dc_launch_events.txt)
     rend.set_timing(False)
-    spec_ms = None
+    if not a.specialize:
+        rend.set_specialize(0)
+    frame0 = rend.render_rows(0, H, max_depth=depth)     # the host's first frame: at once, whatever is loaded
+    torch.cuda.synchronize(dev)
+    first_frame_ms = round((time.perf_counter() - t_up) * 1e3, 1)
+    first_kernel = rend.kernel_info().split("last launch: ")[-1]
+    spec_ms = spec = None
     if a.specialize:
-        t0 = time.perf_counter()
-        rend.set_specialize(1)                            # setup: before the settle / warmup / timed steps
-        spec_ms = round((time.perf_counter() - t0) * 1e3, 1)
+        rend.spec_wait()                                  # setup: before the settle / warmup / timed steps
+        spec_ms = round((time.perf_counter() - t_up) * 1e3, 1)
+        spec = {"request_to_loaded_ms": spec_ms, "first_frame_ms": first_frame_ms, "first_frame_kernel": first_kernel,
+                "generic_ms_per_frame": generic_frame_ms(T, text, t, W, H, depth, local, dev) if world == 1 else None,
+                "note": "RT_OPT_SPECIALIZE 1 (the library default) compiles in a background pool: upload and the first "
+                        "frames return at once on the generic kernels, the specialised kernels take over when loaded "
+                        "(request_to_loaded_ms, the compile plus the load; ~0 with the on-disk or comgr cache warm)"}
+    del frame0
 
     layout = a.layout if multi else "contiguous"
     band = a.band if layout == "cyclic" else -(-H // world)
@@ -539,7 +553,8 @@ def main():
                                     (y_first, band_rows, pitch, n_bands), H, W, world, layout, band, depth,
                                     rehearse, extra_steps, fl0["row_flops"] if fl0 else None)
     elif not multi and K == 1 and not a.no_extra:
-        infl = inflight_phase(T, rend, stream, dev, frames[0], whole, H, W, depth, local, 4, extra_steps)
+        infl = inflight_phase(T, rend, stream, dev, frames[0], whole, H, W, depth, local, 4, max(20, a.steps),
+                              a.settle_ms)
     if rank == 0 and a.png:
         T.write_png(a.png, frames[(a.warmup + a.steps - 1) % nbuf].cpu().numpy())
 
@@ -611,7 +626,13 @@ def main():
         "settle": settle,
         "kernel_code": rend.kernel_info(),
         "spec_compile_ms": spec_ms,
+        "specialisation": spec,
     }
+    if spec and spec.get("generic_ms_per_frame"):
+        g, sp = spec["generic_ms_per_frame"], line["ms_per_step"]
+        spec["specialised_ms_per_frame"] = sp
+        spec["frames_rendered_generic_meanwhile"] = int(spec_ms / g) if g else None
+        spec["break_even_frames_if_blocking"] = int(spec_ms / (g - sp)) if g > sp else None
     if rehearse:
         line.update({"metric": "one-GPU rehearsal of the N-rank pipeline (not a measurement)", "value": None,
                      "vs_baseline": None, "roofline": None, "roofline_hbm": None, "rays": None})
@@ -641,7 +662,28 @@ def main():
         dist.destroy_process_group()
 
 
-def inflight_phase(T, rend, stream, dev, frame, whole, H, W, depth, local, K, steps):
+def generic_frame_ms(T, text, t, W, H, depth, local, dev, frames=10):
+    """Setup, untimed: the generic kernels' wall ms per frame (a context of its own with RT_OPT_SPECIALIZE
+    0; calibration + 3 warm frames first) -- what a host renders at until the specialised program is
+    loaded; with the lines' spec_compile_ms it gives the break-even of a BLOCKING compile."""
+    import torch
+    r = T.Renderer(local, specialize=0)
+    r.upload(T.Scene.compile(text, t, W, H, asset_dir=SCENES))
+    r.set_timing(False)
+    out = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
+    for _ in range(4):
+        r.render_rows(0, H, max_depth=depth, out=out)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        r.render_rows(0, H, max_depth=depth, out=out)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) * 1e3 / frames
+    r.free()
+    return round(ms, 4)
+
+
+def inflight_phase(T, rend, stream, dev, frame, whole, H, W, depth, local, K, steps, settle_ms):
     """N = 1: `steps` frames with K in flight, each stream on a hardware queue of its own and writing
     only its own buffer, the megakernel (as the N > 1 pipeline runs); checked against `whole`."""
     import torch
@@ -651,8 +693,16 @@ def inflight_phase(T, rend, stream, dev, frame, whole, H, W, depth, local, K, st
     rend.set_kernel("mega")
     rend.render_rows(0, H, max_depth=depth, out=bufs[0], stream=stream)      # calibrates this kernel's order
     torch.cuda.synchronize(dev)
-    for i in range(2 * K):
+    # settle, as before the timed region: the calibration's host sort and the set-up above leave the GPU
+    # idle for tens of ms, and a short warm-up then left the clock ramp inside this phase's few timed
+    # frames -- round 4's `inflight4` ran 0.371 ms per frame against 0.324 for lone frames, while the
+    # same arrangement after a settle measures 0.3243 vs 0.3242 (profiles/r07a_inflight_probe.txt)
+    i, ts = 0, time.perf_counter()
+    while i < 2 * K or (time.perf_counter() - ts) * 1e3 < settle_ms:
         rend.render_rows(0, H, max_depth=depth, out=bufs[i % K], stream=ss[i % K])
+        i += 1
+        if i % (8 * K) == 0:
+            torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(steps):
@@ -914,10 +964,10 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
     t0 = time.perf_counter()
     rends = []
     for sc in scenes:
-        r = T.Renderer(local)
+        r = T.Renderer(local, specialize=1 if a.specialize else 0)
+        r.upload(sc)                                      # the frame's family program (compiled above) or its own
         if a.specialize:
-            r.set_specialize(1)
-        r.upload(sc)
+            r.spec_wait()
         r.set_timing(False)                               # bench's own events time the frames
         r.set_kernel(a.kernel)
         rends.append(r)

@@ -9,7 +9,8 @@
  * INTEGRATION.md.
  *
  * Conventions
- *   - every function returns RT_OK (0) or a negative rt_status; none aborts;
+ *   - every function returns RT_OK (0) or a negative rt_status; none aborts (one exception:
+ *     rt_ctx_spec_wait returns RT_PENDING (> 0) when its time limit passes first);
  *     rt_last_error() returns a thread-local message for the last failure;
  *   - no torch / HIP types in signatures: plain pointers, sizes and an opaque
  *     `void* stream` (a hipStream_t; NULL = the device's default stream, as in HIP);
@@ -42,7 +43,8 @@ typedef enum rt_status {
   RT_ERR_IO = -4,           /* texture file missing / undecodable                     */
   RT_ERR_DEVICE = -5,       /* HIP error, no GPU, or kernel launch failure            */
   RT_ERR_UNSUPPORTED = -6,  /* outside this build's limits (e.g. max_depth > 16)      */
-  RT_ERR_NOMEM = -7
+  RT_ERR_NOMEM = -7,
+  RT_PENDING = 1            /* not an error: still in progress (rt_ctx_spec_wait's time limit) */
 } rt_status;
 
 typedef enum rt_csg_op { RT_CSG_UNION = 0, RT_CSG_INTERSECTION = 1, RT_CSG_DIFFERENCE = 2 } rt_csg_op;
@@ -237,7 +239,10 @@ int rt_antialias(rt_ctx* ctx, const uint8_t* src_rgba8, size_t src_stride, doubl
 /* Milliseconds of the last render launch on this context (HIP events recorded on the launch's
  * stream around the kernel; RT_OPT_TIMING 0 turns them off and this call then fails). */
 int rt_ctx_last_kernel_ms(rt_ctx* ctx, float* ms);
-int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launch (which must still exist) */
+/* Waits until every launch this context made has finished, on whichever streams (each launch records
+ * a completion event of the context's own; the callers' streams are never touched, so they may have
+ * been destroyed). */
+int rt_ctx_synchronize(rt_ctx* ctx);
 /* Tuning options of a context.  No option changes a single pixel; they only choose how the
  * kernels run.  RT_OPT_KERNEL selects the render kernel for scenes without a transparent object:
  *   RT_KERNEL_AUTO (default): a launch bound by its costliest tiles (fewer tiles than ~5 per wave
@@ -270,35 +275,64 @@ int rt_ctx_synchronize(rt_ctx* ctx);   /* waits for the stream of the last launc
  * recursion level (it reads each level's ray count), and RT_KERNEL_AUTO's first ordered launch of a
  * ray-tree geometry times one wavefront launch against the megakernel (blocking, once): such
  * launches return only after the work is done, even with device output.
- * RT_OPT_SPECIALIZE: 0 (default) the library's precompiled kernels; 1 also compiles the uploaded
- * scene's row kernels with the scene's tables as constants (hipRTC, spec.hip: the hierarchy walk
- * unrolled, every record field a literal; same pixels) for RGBA8 / RGB8 launches; 2 for the f64
- * and calibration launches too.  The compile runs on the calling thread at
- * rt_ctx_upload (or here, when a scene is already uploaded): seconds of host time per new scene (the
- * code object is cached per process by the program text), so it pays for hosts that render many
- * frames of one scene.  Scenes of more than 32 objects or 48 leaves keep the generic kernels (the
- * unrolled walks grow with the scene; rt_ctx_kernel_info says so).  Launches whose kernel has no specialised form (wavefront, refraction
- * deferred, RT_OPT_FAST_CLAMP 0 on a min/max-clamp scene) keep the generic kernels.
- * RT_OPT_TAIL_TILES: tail-bound launches of scenes without a transparent object (the deferred
- * kernel's ordered launches, RGBA8 / RGB8) take their costliest calibrated tiles out of the main
- * launch and render them in a kernel of their own, started first on an internal stream with a
- * hardware queue of its own, several lanes tracing each pixel's rays together; this many tiles
- * (default 0 = none; at most an eighth of the launch's).  Same pixels. */
+ * RT_OPT_SPECIALIZE: 1 (default) compiles the uploaded scene's row kernels once more with the scene's
+ * tables as constants (hipRTC, spec.hip: the hierarchy walk unrolled, every record field a literal;
+ * same pixels) for RGBA8 / RGB8 launches; 2 for the f64 and calibration launches too; 0 never.  The
+ * compile is ASYNCHRONOUS: rt_ctx_upload (or this call) requests it from a pool of library threads
+ * and returns at once; launches take the generic kernels until the code objects are ready and the
+ * specialised ones from the first launch after (rt_ctx_kernel_info says which ran).  The first frame
+ * therefore renders as fast as without the option, and the compile (seconds of host time on a new
+ * scene; 4K globes: 0.457 -> 0.325 ms per frame once loaded) costs the host thread nothing.
+ * rt_ctx_spec_wait blocks for it.  Programs are cached per process by their full text, and on disk
+ * (rt_spec_cache_dir) by text and compiler.  Scenes of more than 32 objects or 48 leaves keep the
+ * generic kernels (the unrolled walks grow with the scene), and so does a context whose compile
+ * failed or whose code object exceeds the resource guard, or when the ROCm installation's hipRTC
+ * cannot be loaded (rt_ctx_kernel_info says why; the upload itself succeeds).  Setting the same
+ * value again after a failure retries the compile.  Launches whose kernel has no specialised form
+ * (wavefront, refraction deferred, RT_OPT_FAST_CLAMP 0 on a min/max-clamp scene) keep the generic
+ * kernels.
+ * RT_OPT_TILES_PER_WAVE: the specialised megakernel takes its 8x8 tiles grid-stride, this many per
+ * wave (1..16); 0 (default) lets the calibration choose from the launch's tile costs (cheap launches,
+ * e.g. primary rays only, take several: a wave's dispatch then serves more pixels).  Same pixels.
+ * Option 7 is retired (round 4's tail kernel, measured slower than the launch it shortened). */
 typedef enum rt_option {
   RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4,
-  RT_OPT_WAVEFRONT_PAIRS = 5, RT_OPT_SPECIALIZE = 6, RT_OPT_TAIL_TILES = 7
+  RT_OPT_WAVEFRONT_PAIRS = 5, RT_OPT_SPECIALIZE = 6, RT_OPT_TILES_PER_WAVE = 8
 } rt_option;
 typedef enum rt_kernel_choice {
   RT_KERNEL_AUTO = 0, RT_KERNEL_MEGA = 1, RT_KERNEL_DEFERRED = 2, RT_KERNEL_WAVEFRONT = 3
 } rt_kernel_choice;
 int rt_ctx_set_option(rt_ctx* ctx, int32_t option, int32_t value);
-/* What the context's row launches run, as text: "generic (librt_mi355x.so)" or the specialised
- * program's hash, mode and compile time, and which kernel the last row launch took. */
+/* What the context's row launches run, as text: "generic (librt_mi355x.so...)" -- with the reason when
+ * RT_OPT_SPECIALIZE is on (compiling in the background, failed, scene too large) -- or the specialised
+ * program's hash, mode, compile time, compiler and resources, and which kernel the last row launch took. */
 int rt_ctx_kernel_info(rt_ctx* ctx, char* buf, size_t cap);
+/* Block until the context's specialised program (RT_OPT_SPECIALIZE) is loaded, at most timeout_ms
+ * (< 0: no limit).  RT_OK: loaded, or nothing to wait for (option off, scene too large); RT_PENDING:
+ * the limit passed first; a negative status: the compile failed or the guard refused it (the
+ * context keeps the generic kernels, rt_last_error / rt_ctx_kernel_info say why). */
+int rt_ctx_spec_wait(rt_ctx* ctx, int32_t timeout_ms);
 /* Compile the scene's specialised program (RT_OPT_SPECIALIZE) into the process's code-object
  * cache without a device, so a later upload of the same scene finds it; *compile_ms = the hipRTC
  * time (0 when it was cached already).  May run on any thread. */
 int rt_scene_precompile(const rt_scene* scene, double* compile_ms);
+/* rt_scene_precompile, then a report of the programs as text (cap, len as rt_scene_describe): the
+ * compiler's identity, and per kernel "NAME: vgprs V spilled S sgprs G scratch B occupancy W code N
+ * compile_ms T source hiprtc|disk" (the code object's metadata: what the resource guard checks). */
+int rt_scene_spec_report(const rt_scene* scene, char* buf, size_t cap, size_t* len);
+/* The hipRTC the programs compile with (its path, version, real path, size and mtime: the disk-cache
+ * key), and *rocm = 1 when it is the ROCm installation's own ($ROCM_PATH or /opt/rocm), loaded into a
+ * link-map namespace of its own; 0 when that failed (then nothing is specialised: the process's own
+ * hipRTC may be another LLVM -- PyTorch bundles one -- whose code ran 19x slower). */
+int rt_spec_compiler_info(char* buf, size_t cap, int32_t* rocm);
+/* The on-disk code-object cache of the specialised programs: a directory (created on first write);
+ * NULL or "" (the default) for none.  Entries are keyed by the full program text and the compiler's
+ * identity, and both are compared on a hit. */
+int rt_spec_cache_dir(const char* dir);
+/* Stop the compile pool before the process exits: queued compiles are cancelled, running ones are
+ * waited for (a compile still running in a library thread while the process tears hipRTC down could
+ * crash the exit).  Later requests fail (contexts keep the generic kernels). */
+void rt_spec_shutdown(void);
 /* The specialised program's text (tests, debugging): cap, len as rt_scene_describe. */
 int rt_scene_spec_program(const rt_scene* scene, char* buf, size_t cap, size_t* len);
 /* Specialised programs for n scenes -- the frames of an animation (the reference's animate mode

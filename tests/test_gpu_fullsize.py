@@ -99,19 +99,52 @@ def test_globes4k_rank_bands_full_frame(T, globes4k_oracle, world, channels):
     assert_close(frames[1], None, globes4k_oracle, None, f"4K globes N={world} bands, ordered launches")
 
 
-@pytest.mark.parametrize("chunk", list(range(8)))
-def test_spinning_globes_animation_frames(T, chunk):
-    """BASELINE config 5, ALL 120 frames (15 per test case): frame f at time f / 120, 1920x1080,
-    depth 10 (refraction chains), each through its calibration launch and the cost-ordered launch
-    that follows, against the oracle frame (the reference's per-frame scene build,
-    src/raydebugger/debug_window.rs:53-62, and render, raytracer.rs:132-287)."""
+@pytest.fixture(scope="module")
+def anim_families(T):
+    """The scene families exactly as `bench.py --config anim120` registers them: all 120 frames of
+    spinning_globes.scene at 1920x1080, time f / 120 (rt_spec_family_register; two families, 63 + 57
+    frames).  Yields the family size each frame's program must report."""
     text = scene_text("spinning_globes")
+    scenes = [T.Scene.compile(text, f / 120, 1920, 1080, asset_dir=SCENES) for f in range(120)]
+    T.Scene.clear_families()
+    T.Scene.register_family(scenes)
+    yield text
+    T.Scene.clear_families()
+
+
+@pytest.mark.parametrize("chunk", list(range(8)))
+def test_spinning_globes_animation_frames(T, anim_families, chunk):
+    """BASELINE config 5, ALL 120 frames (15 per test case): frame f at time f / 120, 1920x1080,
+    depth 10 (refraction chains), against the oracle frame (the reference's per-frame scene build,
+    src/raydebugger/debug_window.rs:53-62, and render, raytracer.rs:132-287), through BOTH code paths
+    the library has for it:
+      * the generic chain megakernel: calibration launch, then the cost-ordered launch;
+      * the code objects `bench.py --config anim120` times: the frame's scene-family program
+        (RT_OPT_SPECIALIZE 1 after the bench's own 120-frame registration, `anim_families`) -- the
+        ordered launch is the family's specialised megakernel, and the kernel info must name a family
+        of 63 or 57 frames."""
+    import torch
+    text = anim_families
     W, H = 1920, 1080
+    families = set()
     for frame in range(chunk * 15, chunk * 15 + 15):
-        cal, ordered = gpu_frames(T, text, frame / 120, W, H, 10)
         ref = oracle_frame(text, frame / 120, W, H, 10)
+        cal, ordered = gpu_frames(T, text, frame / 120, W, H, 10)
         assert_close(cal, None, ref, None, f"spinning_globes f={frame} calibration launch")
         assert_close(ordered, None, ref, None, f"spinning_globes f={frame} ordered launch")
+        r = T.Renderer(0)
+        r.set_specialize(1)
+        r.upload(T.Scene.compile(text, frame / 120, W, H, asset_dir=SCENES))
+        r.set_timing(False)
+        for launch in ("calibration", "ordered"):
+            f = r.render_rows(0, H, max_depth=10)
+            torch.cuda.synchronize()
+            info = r.kernel_info()
+            assert_close(f.cpu().numpy(), None, ref, None, f"spinning_globes f={frame} family program, {launch} ({info})")
+        assert "megakernel (specialised)" in info and ("family of 63 scenes" in info or "family of 57 scenes" in info), info
+        families.add(info.split("family of ")[1].split(" ")[0])
+        r.free()
+    print(f"frames {chunk * 15}..{chunk * 15 + 14}: families {sorted(families)}")
 
 
 def test_dsl_quirk_scenes_through_product_compiler(T):

@@ -67,6 +67,24 @@ def test_globes4k_rank_bands_specialised(worldmap, world):
     assert any("specialised" in k for k in kinds), kinds
 
 
+def test_sphere1080_d0_specialised_full_frame():
+    """BASELINE config 2 as `bench.py --config sphere1080d0` runs it (RT_OPT_SPECIALIZE 1, timing
+    events off): the calibration launch and the cost-ordered launches of the specialised megakernel,
+    1920x1080 primary rays only, every pixel against the oracle."""
+    import torch
+    W, H = 1920, 1080
+    text = "draw(sphere(<0, 0, 0>, 30, red))"
+    rt, r = _renderer(text, 0.0, W, H, 0, 1)
+    r.set_timing(False)
+    _, ref = _oracle(text, 0.0, W, H, 0)
+    for launch in ("calibration", "ordered", "ordered again"):
+        f = r.render_rows(0, H, max_depth=0)
+        torch.cuda.synchronize()
+        info = r.kernel_info()
+        assert_close(f.cpu().numpy(), None, ref, None, f"spec sphere 1080p d0 {launch} launch ({info})")
+    assert "megakernel (specialised)" in info, info
+
+
 @pytest.mark.parametrize("kernel", ["auto", "deferred", "mega"])
 def test_globes1080_d5_specialised(worldmap, kernel):
     import torch

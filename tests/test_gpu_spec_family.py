@@ -31,7 +31,8 @@ def _render(text, t):
     sc = T.Scene.compile(text, t, W, H, asset_dir=SCENES)
     r = T.Renderer(0)
     r.set_specialize(1)
-    r.upload(sc)
+    r.upload(sc)                       # requests the program: a registered family's (compiled), or its own
+    r.spec_wait()
     frames = [r.render_rows_host(0, H) for _ in range(2)]          # calibration, then the ordered launch
     return frames, r.kernel_info()
 
@@ -64,4 +65,5 @@ def test_other_scene_keeps_its_program(worldmap, family):
     r = T.Renderer(0)
     r.set_specialize(1)
     r.upload(sc)
+    r.spec_wait()
     assert r.kernel_variant() == "spec" and "family" not in r.kernel_info(), r.kernel_info()

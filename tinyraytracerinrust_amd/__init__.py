@@ -21,6 +21,8 @@ from .raytracer import (  # noqa: F401
     TransformationStack,
     device_count,
     read_png_rgba8,
+    spec_cache_dir,
+    spec_compiler_info,
     solid_material,
     textured_material,
     write_png,
@@ -28,6 +30,6 @@ from .raytracer import (  # noqa: F401
 
 __all__ = [
     "RtError", "lib", "MAX_FRAMES", "ORTHO_SCALE", "AntiAliaser", "HwStream", "OrthoAxes", "RAY_RECORD_DTYPE", "RayDebugger", "MatrixTransformation", "RayTracer", "Renderer", "Scene",
-    "TransformationStack", "device_count", "read_png_rgba8", "solid_material", "textured_material",
+    "TransformationStack", "device_count", "read_png_rgba8", "spec_cache_dir", "spec_compiler_info", "solid_material", "textured_material",
     "write_png",
 ]

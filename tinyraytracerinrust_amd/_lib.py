@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RT_LIB_PATH") or os.path.join(HERE, "librt_mi355x.so")
 
 RT_OK = 0
+RT_PENDING = 1          # rt_ctx_spec_wait: the time limit passed before the compile finished (not an error)
 STATUS_NAMES = {
     0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_PARSE", -3: "RT_ERR_EVAL", -4: "RT_ERR_IO",
     -5: "RT_ERR_DEVICE", -6: "RT_ERR_UNSUPPORTED", -7: "RT_ERR_NOMEM",
@@ -26,7 +27,7 @@ RT_OPT_FAST_CLAMP = 3
 RT_OPT_WAVEFRONT_CAP = 4
 RT_OPT_WAVEFRONT_PAIRS = 5
 RT_OPT_SPECIALIZE = 6
-RT_OPT_TAIL_TILES = 7
+RT_OPT_TILES_PER_WAVE = 8
 RT_KERNEL_AUTO, RT_KERNEL_MEGA, RT_KERNEL_DEFERRED, RT_KERNEL_WAVEFRONT = 0, 1, 2, 3
 
 
@@ -84,6 +85,11 @@ SIGNATURES = {
     "rt_spec_family_register": (_I, [ctypes.POINTER(_P), ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]),
     "rt_spec_family_clear": (_I, []),
     "rt_ctx_kernel_info": (_I, [_P, ctypes.c_char_p, ctypes.c_size_t]),
+    "rt_ctx_spec_wait": (_I, [_P, ctypes.c_int32]),
+    "rt_scene_spec_report": (_I, [_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+    "rt_spec_compiler_info": (_I, [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32)]),
+    "rt_spec_cache_dir": (_I, [ctypes.c_char_p]),
+    "rt_spec_shutdown": (None, []),
     "rt_scene_info": (_I, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_U32),
                            ctypes.POINTER(_U32)]),
@@ -148,6 +154,13 @@ def lib() -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     _lib = handle
+    # The on-disk cache of scene-specialised code objects (rt_spec_cache_dir; keyed and checked by
+    # program text and compiler): ~/.cache/tinyraytracerinrust_amd/spec, or RT_SPEC_CACHE_DIR
+    # ("" turns it off).  The C library itself keeps none unless its host asks.
+    cache = os.environ.get("RT_SPEC_CACHE_DIR")
+    if cache is None:
+        cache = os.path.join(os.path.expanduser("~"), ".cache", "tinyraytracerinrust_amd", "spec")
+    handle.rt_spec_cache_dir(cache.encode())
     return handle
 
 

@@ -82,7 +82,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   if (max_depth > RT_MAX_DEPTH_CAP) return fail(RT_ERR_UNSUPPORTED, "max_depth %d > %d", max_depth, RT_MAX_DEPTH_CAP);
   RT_HIP(hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;   // NULL = the device's default stream
-  c->stream = st;
+  (void)spec_poll(c);                     // the scene-specialised kernels, once their background compile is done
   const bool dev_out = is_device_ptr(out);
   uint8_t* target = (uint8_t*)out;
   size_t tstride = stride;
@@ -104,6 +104,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     c->last_kernel = "wavefront";
     if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
     c->timed = c->timing;
+    RT_TRY(mark_launch(c, st));
     if (!dev_out) {
       RT_HIP(hipMemcpy2DAsync(out, stride, target, tstride, row_bytes, n_rows, hipMemcpyDeviceToHost, st));
       RT_HIP(hipStreamSynchronize(st));
@@ -188,6 +189,7 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     c->last_kernel = "wavefront";
     if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
     c->timed = c->timing;
+    RT_TRY(mark_launch(c, st));
     if (!dev_out) {
       RT_HIP(hipMemcpy2DAsync(out, stride, target, tstride, row_bytes, n_rows, hipMemcpyDeviceToHost, st));
       RT_HIP(hipStreamSynchronize(st));
@@ -202,33 +204,17 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   if (c->spec_mod && mode == c->spec_mode && fc == c->spec_fc)
     sfn = deferred ? c->spec_def[f64 ? 1 : 0][calibrate ? 1 : 0] : c->spec_rows[f64 ? 1 : 0][calibrate ? 1 : 0];
   c->last_kernel = deferred ? (sfn ? "deferred (specialised)" : "deferred") : (sfn ? "megakernel (specialised)" : "megakernel");
-  // the tail kernel first, on its own hardware queue, concurrently with the main launch (which then
-  // waits for it on the caller's stream): the costliest tiles' chains start at once, G lanes per pixel
-  const bool tail = order && deferred && slot->n_tail > 0;
-  if (tail) {
-    if (!c->tail_stream) {
-      hipDeviceProp_t prop;
-      RT_HIP(hipGetDeviceProperties(&prop, c->device));
-      std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0xFFFFFFFFu);
-      if (prop.multiProcessorCount % 32) mask.back() = (1u << (prop.multiProcessorCount % 32)) - 1u;
-      RT_HIP(hipExtStreamCreateWithCUMask(&c->tail_stream, (uint32_t)mask.size(), mask.data()));
-      RT_HIP(hipEventCreateWithFlags(&c->tail_ev0, hipEventDisableTiming));
-      RT_HIP(hipEventCreateWithFlags(&c->tail_ev1, hipEventDisableTiming));
-    }
-    RT_HIP(hipEventRecord(c->tail_ev0, st));
-    RT_HIP(hipStreamWaitEvent(c->tail_stream, c->tail_ev0, 0));
-    const int rc = launch_tail(c, c->tail_stream, slot->n_tail, a0, a1, a2, a3, max_depth, target, tstride, slot->d_tail,
-                               rgbi, fc);
-    if (rc) return rc;
-    hipStream_t ts = c->tail_stream;
-    RT_HIP(hipGetLastError());
-    RT_HIP(hipEventRecord(c->tail_ev1, ts));
-    c->last_kernel = sfn ? "tail + deferred (specialised)" : "tail + deferred";
-  }
   if (sfn) {
+    // the specialised megakernel takes its entries grid-stride: `tpw` entries per wave for launches
+    // whose tiles are cheap (RT_OPT_TILES_PER_WAVE; the calibration's choice by default)
+    unsigned n_entries = grid.x, wgs = grid.x;
+    if (!deferred) {
+      const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : slot && slot->valid && !calibrate ? slot->tpw : 1;
+      wgs = (n_entries + (unsigned)tpw - 1) / (unsigned)tpw;
+    }
     void* kargs[] = {&c->dev, (void*)&a0, (void*)&a1, (void*)&a2, (void*)&a3, &max_depth, &target, &tstride,
-                     (void*)&order, &cost, (void*)&rgbi};
-    RT_HIP(hipModuleLaunchKernel(sfn, grid.x, 1, 1, 64, 1, 1, 0, st, kargs, nullptr));
+                     (void*)&order, &cost, (void*)&rgbi, &n_entries};
+    RT_HIP(hipModuleLaunchKernel(sfn, wgs, 1, 1, 64, 1, 1, 0, st, kargs, nullptr));
   }
   else if (deferred && chain && f64) { RT_LAUNCH_DEFERRED(true, true) }
   else if (deferred && chain) { RT_LAUNCH_DEFERRED(false, true) }
@@ -243,9 +229,9 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
 #undef RT_LAUNCH_ROWS
 #undef RT_LAUNCH_DEFERRED
   RT_HIP(hipGetLastError());
-  if (tail) RT_HIP(hipStreamWaitEvent(st, c->tail_ev1, 0));
   if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
   c->timed = c->timing;
+  RT_TRY(mark_launch(c, st));
   if (tune) {                         // synchronous, once per ray-tree geometry (see above)
     float mega_ms = 0.0f, wf_ms = 0.0f;
     RT_HIP(hipEventRecord(c->tev1, st));
@@ -304,18 +290,9 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
       std::vector<uint32_t> sorted_cost(h_cost);
       std::nth_element(sorted_cost.begin(), sorted_cost.begin() + n_tiles / 2, sorted_cost.end());
       const double med = std::max(1.0, (double)sorted_cost[n_tiles / 2]);
-      // the costliest tiles go to the tail kernel (reflection-only scenes, RGBA8 / RGB8 launches): at most
-      // an eighth of the launch, never the whole launch
-      size_t n_tail = 0;
-      if (!refr && !f64 && c->tail_tiles > 0 && n_tiles >= 16 && c->tbl_bytes <= RT_TAIL_MAX_TABLE_BYTES) {
-        n_tail = std::min<size_t>((size_t)c->tail_tiles, n_tiles / 8);
-        RT_HIP(hipMalloc((void**)&slot->d_tail, n_tail * sizeof(int32_t)));
-        RT_HIP(hipMemcpy(slot->d_tail, h_order.data(), n_tail * sizeof(int32_t), hipMemcpyHostToDevice));
-        slot->n_tail = (uint32_t)n_tail;
-      }
       std::vector<int32_t> split;
       split.reserve(n_tiles + n_tiles / 8);
-      for (size_t i = n_tail; i < n_tiles; ++i) {
+      for (size_t i = 0; i < n_tiles; ++i) {
         const uint32_t t = (uint32_t)h_order[i];
         int lp = 0;
         while (lp < RT_SPLIT_MAX_LOG2 && h_cost[t] >= split_k * med * (double)(2 << lp)) ++lp;

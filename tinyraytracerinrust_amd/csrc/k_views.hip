@@ -421,7 +421,6 @@ int rt_antialias(rt_ctx* c, const uint8_t* src_rgba8, size_t src_stride, double 
   if (dst_f64 && f64_stride < row32) return fail(RT_ERR_INVALID, "f64 stride %zu < %zu", f64_stride, row32);
   RT_HIP(hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
-  c->stream = st;
   const size_t npx = (size_t)W * H;
   // device staging: [src u8][dst u8][dst f64][edges][counters] for host pointers
   const bool d_src = is_device_ptr(src_rgba8), d_u8 = !dst_rgba8 || is_device_ptr(dst_rgba8);
@@ -500,6 +499,7 @@ int rt_antialias(rt_ctx* c, const uint8_t* src_rgba8, size_t src_stride, double 
   }
   if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
   c->timed = c->timing;
+  RT_TRY(rt::mark_launch(c, st));
   if (dst_rgba8 && !d_u8) RT_HIP(hipMemcpy2DAsync(dst_rgba8, dst_stride, u8, row4, row4, H, hipMemcpyDeviceToHost, st));
   if (dst_f64 && !d_f64) RT_HIP(hipMemcpy2DAsync(dst_f64, f64_stride, f64, row32, row32, H, hipMemcpyDeviceToHost, st));
   RT_HIP(hipStreamSynchronize(st));
@@ -529,7 +529,6 @@ int rt_render_ortho(rt_ctx* c, int32_t axis1, int32_t axis2, double dir1, double
   if (rgba_f64 && f64_stride < row32) return fail(RT_ERR_INVALID, "f64 stride %zu < %zu", f64_stride, row32);
   RT_HIP(hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
-  c->stream = st;
   const bool d8 = !rgba8 || is_device_ptr(rgba8), df = !rgba_f64 || is_device_ptr(rgba_f64);
   uint8_t* t8 = rgba8;
   double* tf = rgba_f64;
@@ -547,6 +546,7 @@ int rt_render_ortho(rt_ctx* c, int32_t axis1, int32_t axis2, double dir1, double
   RT_HIP(hipGetLastError());
   if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
   c->timed = c->timing;
+  RT_TRY(rt::mark_launch(c, st));
   if (!d8) RT_HIP(hipMemcpy2DAsync(rgba8, row_stride_bytes, t8, row4, row4, n, hipMemcpyDeviceToHost, st));
   if (!df) RT_HIP(hipMemcpy2DAsync(rgba_f64, f64_stride, tf, row32, row32, n, hipMemcpyDeviceToHost, st));
   if (!d8 || !df) RT_HIP(hipStreamSynchronize(st));
@@ -573,12 +573,12 @@ int rt_record_rays(rt_ctx* c, double x, double y, int32_t max_depth, rt_ray_reco
   int* d_ord = (int*)(sb + ord_off);
   int* d_cnt = (int*)(sb + cnt_off);
   hipStream_t st = nullptr;
-  c->stream = st;
   if (refr)
     hipLaunchKernelGGL((record_ray_kernel<true>), dim3(1), dim3(64), 0, st, c->dev, x, y, (int)max_depth, d_rec, d_ord, dev_cap, d_cnt);
   else
     hipLaunchKernelGGL((record_ray_kernel<false>), dim3(1), dim3(64), 0, st, c->dev, x, y, (int)max_depth, d_rec, d_ord, dev_cap, d_cnt);
   RT_HIP(hipGetLastError());
+  RT_TRY(rt::mark_launch(c, st));
   int cnt[2] = {0, 0};
   RT_HIP(hipMemcpy(cnt, d_cnt, sizeof cnt, hipMemcpyDeviceToHost));
   if (cnt[0] != cnt[1] || cnt[1] > dev_cap) return fail(RT_ERR_DEVICE, "ray recorder overflow (%d/%d of %d)", cnt[0], cnt[1], dev_cap);
@@ -608,6 +608,7 @@ int rt_trace_pixel_f64(const rt_scene* scene, double x, double y, int32_t max_de
     int rc = rt_ctx_create(device, &h.c);
     if (rc) return rc;
     rt_ctx_set_option(h.c, RT_OPT_TIMING, 0);
+    rt_ctx_set_option(h.c, RT_OPT_SPECIALIZE, 0);   // one point per upload: never worth a compile
   }
   int rc = rt_ctx_upload(h.c, scene);
   if (rc) return rc;
@@ -623,7 +624,6 @@ int rt_render_points_f64(rt_ctx* c, const double* xy, size_t n, int32_t max_dept
   if (n == 0) return RT_OK;
   RT_HIP(hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;   // NULL = the device's default stream
-  c->stream = st;
   const bool dev_in = is_device_ptr(xy), dev_out = is_device_ptr(out);
   const double* in = xy;
   double* target = out;
@@ -641,6 +641,7 @@ int rt_render_points_f64(rt_ctx* c, const double* xy, size_t n, int32_t max_dept
   RT_HIP(hipGetLastError());
   if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
   c->timed = c->timing;
+  RT_TRY(rt::mark_launch(c, st));
   if (!dev_out) {
     RT_HIP(hipMemcpyAsync(out, target, n * 4 * sizeof(double), hipMemcpyDeviceToHost, st));
     RT_HIP(hipStreamSynchronize(st));

@@ -13,9 +13,10 @@
 #include "rt_blob.h"
 #include "scene.h"
 
+namespace rt { struct SpecJob; }        // spec.hip: one program's compile, shared by the contexts that want it
+
 struct rt_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;       // last stream launched on (NULL = the default stream)
   void* d_blob = nullptr;
   size_t blob_bytes = 0;
   RtDevScene dev;
@@ -24,6 +25,7 @@ struct rt_ctx {
   bool timing = true;                   // rt_ctx_set_option(RT_OPT_TIMING): launch events recorded
   bool tile_order = true;               // rt_ctx_set_option(RT_OPT_TILE_ORDER): cost-ordered dispatch
   bool fast_clamp = true;               // rt_ctx_set_option(RT_OPT_FAST_CLAMP): min/max clamps where exact
+  int tiles_per_wave = 0;               // rt_ctx_set_option(RT_OPT_TILES_PER_WAVE): 0 auto (calibration), 1..16
   int wf_cap_pct = 200;                 // rt_ctx_set_option(RT_OPT_WAVEFRONT_CAP): rays per level, % of pixel slots
   double wf_klo[3] = {-100, -100, -100}, wf_khi[3] = {100, 100, 100};   // coherence-key extent (bounded objects)
   int n_cu = 256;                       // compute units of the device (wave slots = n_cu x 4 SIMDs x waves/SIMD)
@@ -58,16 +60,16 @@ struct rt_ctx {
     bool deferred = false;            // ordered launches take the deferred-shadow kernel
     int wf_tune = 0;                  // ray-tree scenes, RT_KERNEL_AUTO: 0 not yet timed, 1 megakernel, 2 wavefront
     bool valid = false;               // set once the sorted order is on the device
-    int32_t* d_tail = nullptr;        // deferred launches of reflection-only scenes: the costliest tiles, rendered by
-    uint32_t n_tail = 0;              //   the tail kernel (G lanes per pixel) on tail_stream, not by the main launch
+    int tpw = 1;                      // entries per wave of the specialised megakernel (cheap tiles: several)
   };
   static constexpr int RT_ORDER_SLOTS = 8;
   OrderSlot order[RT_ORDER_SLOTS];
   uint64_t use_clock = 0;
   // Scene-specialised row kernels (spec.hip, rt_ctx_set_option(RT_OPT_SPECIALIZE)): hipRTC compiles
-  // rt_device.h with this scene's tables as constexpr data; launches take them when they match.
-  int spec_on = 0;                      // RT_OPT_SPECIALIZE: 0 off, 1 product launches, 2 every row launch
-  std::string spec_src;                 // the program text of the uploaded scene (spec_source)
+  // rt_device.h with this scene's tables as constexpr data, in the background (the library's compile
+  // pool); launches take them once they are loaded (spec_poll), the generic kernels until then.
+  int spec_on = 1;                      // RT_OPT_SPECIALIZE: 0 off, 1 (default) product launches, 2 every row launch
+  std::string spec_src;                 // the program's prelude (spec_source, or a registered family's)
   int spec_mode = 0;                    // RT_MODE_* of the uploaded scene
   bool spec_fc = false;                 // the program's clamp form (RtDevScene::colour_fast)
   bool spec_deferred = false;           // the program also holds the deferred kernels
@@ -76,16 +78,23 @@ struct rt_ctx {
   hipModule_t spec_mods[8] = {};        // one module per specialised kernel, on this context's device
   hipFunction_t spec_rows[2][2] = {};   // [f64][cal]
   hipFunction_t spec_def[2][2] = {};    // [f64][cal]
-  uint64_t spec_hash = 0;               // FNV-1a of the program text (the code-object cache key)
-  double spec_compile_ms = 0.0;         // 0 when the code object came from the process cache
+  uint64_t spec_hash = 0;               // FNV-1a of the prelude (kernel info only; caches compare full texts)
+  double spec_compile_ms = 0.0;         // the hipRTC time of the loaded programs (0: read from the disk cache)
   int spec_family = 0;                  // > 0: the program of a registered scene family of that many members
   std::shared_ptr<rt::FlatScene> spec_flat;   // the uploaded scene's tables (texels dropped): the program is
-                                        // re-chosen when the option is set (families registered since)
+                                        // chosen when the option is set (families registered since the upload)
+  std::vector<std::shared_ptr<rt::SpecJob>> spec_jobs;   // programs requested, not yet loaded (one per kernel)
+  std::string spec_error;               // why the context keeps the generic kernels although spec_on (kernel info)
+  std::string spec_note;                // " [process cache]" / " [disk cache]"
+  std::string spec_res;                 // the loaded megakernel's resources (kernel info)
+  double spec_t0 = 0.0;                 // when the programs were requested (steady clock, ms)
+  double spec_ready_ms = 0.0;           // request -> loaded, ms
+  // Completion marks: per stream this context launched on, an event recorded after its last launch
+  // there.  rt_ctx_synchronize / option changes / rt_ctx_free wait on them -- never on a caller's
+  // stream, which may be destroyed by then.
+  struct Mark { hipStream_t s; hipEvent_t ev; };
+  std::vector<Mark> marks;
   const char* last_kernel = "none";     // what the last row launch ran (rt_ctx_kernel_info)
-  int tail_tiles = 0;                   // rt_ctx_set_option(RT_OPT_TAIL_TILES): tiles the tail kernel takes (0: none)
-  size_t tbl_bytes = 0;                 // the blob's tables [objects, texels): what the tail kernel stages in LDS
-  hipStream_t tail_stream = nullptr;    // the tail kernel's stream (a hardware queue of its own), made on first use
-  hipEvent_t tail_ev0 = nullptr, tail_ev1 = nullptr;
 };
 
 using rt::fail;
@@ -96,9 +105,15 @@ using rt::fail;
     if (e_ != hipSuccess) return fail(RT_ERR_DEVICE, "%s failed: %s", #call, hipGetErrorString(e_)); \
   } while (0)
 
-#define RT_TAIL_MAX_TABLE_BYTES (48 * 1024)
+#define RT_TRY(call)                                                                   \
+  do {                                                                                 \
+    const int rc_ = (call);                                                            \
+    if (rc_) return rc_;                                                               \
+  } while (0)
+
 #define RT_SPEC_MAX_OBJECTS 32
 #define RT_SPEC_MAX_LEAVES 48
+#define RT_SPEC_MAX_FAMILIES 16
 
 namespace rt {
 // rt_ctx.hip
@@ -114,13 +129,15 @@ bool diag_env(const char* name);
 // k_wavefront.hip: the wavefront path for rows (y_first, band_rows, band_pitch, n_rows) = a0..a3
 int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int a3, int max_depth, uint8_t* target,
                      size_t tstride, bool f64, int rgbi, size_t n_tiles);
-// k_tail.hip: the tail kernel over n_tail tiles (their indices in d_tail) on stream st
-int launch_tail(rt_ctx* c, hipStream_t st, uint32_t n_tail, int a0, int a1, int a2, int a3, int max_depth,
-                uint8_t* target, size_t tstride, const int32_t* d_tail, int rgbi, bool fc);
-// spec.hip: the specialised program of a flattened scene (at upload), its build (hipRTC, cached per
-// process, module loaded on the context's device) and release
-void spec_program(const FlatScene& f, rt_ctx* c);   // the scene's mode, clamp form and program text
-int spec_build(rt_ctx* c);
-void spec_drop(rt_ctx* c);
+// Completion marks (rt_ctx.hip): record one after every launch of the context on stream st; wait for all
+int mark_launch(rt_ctx* c, hipStream_t st);
+int wait_launches(rt_ctx* c);
+// spec.hip: the specialised programs of the uploaded scene -- flags (at upload, cheap), the request to the
+// compile pool (asynchronous), the load once compiled (at the next launch, or spec_wait), release
+void spec_flags(const FlatScene& f, rt_ctx* c);     // the scene's mode, clamp form, size limits
+void spec_prepare(rt_ctx* c, bool retry = false);   // request c's programs (spec_on, spec_flat); returns at once
+int spec_poll(rt_ctx* c);                           // load them if compiled: RT_OK, or RT_PENDING (spec_error on failure)
+int spec_wait(rt_ctx* c, double timeout_ms);        // block (< 0: no limit) then spec_poll
+void spec_drop(rt_ctx* c);                          // unload + release (no launch of c may be in flight)
 const char* spec_compiler();                        // which hipRTC compiles the programs
 }  // namespace rt

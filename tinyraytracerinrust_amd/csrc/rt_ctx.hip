@@ -23,7 +23,6 @@ bool diag_env(const char* name) {
 void drop_order(rt_ctx::OrderSlot& s) {
   if (s.d_order) (void)hipFree(s.d_order);     // hipFree waits for work that may still read it
   if (s.d_cost) (void)hipFree(s.d_cost);
-  if (s.d_tail) (void)hipFree(s.d_tail);
   s = rt_ctx::OrderSlot();
 }
 void drop_orders(rt_ctx* c) {
@@ -37,6 +36,30 @@ int ensure_scratch(rt_ctx* c, size_t bytes) {
   c->scratch_bytes = 0;
   RT_HIP(hipMalloc(&c->scratch, bytes));
   c->scratch_bytes = bytes;
+  return RT_OK;
+}
+
+int mark_launch(rt_ctx* c, hipStream_t st) {
+  for (auto& m : c->marks)
+    if (m.s == st) {
+      RT_HIP(hipEventRecord(m.ev, st));
+      return RT_OK;
+    }
+  rt_ctx::Mark m{st, nullptr};
+  if (c->marks.size() >= 16) {        // many streams: the oldest mark's launches are waited for, its event reused
+    m.ev = c->marks.front().ev;
+    RT_HIP(hipEventSynchronize(m.ev));
+    c->marks.erase(c->marks.begin());
+  } else {
+    RT_HIP(hipEventCreateWithFlags(&m.ev, hipEventDisableTiming));
+  }
+  c->marks.push_back(m);
+  RT_HIP(hipEventRecord(m.ev, st));
+  return RT_OK;
+}
+
+int wait_launches(rt_ctx* c) {
+  for (auto& m : c->marks) RT_HIP(hipEventSynchronize(m.ev));
   return RT_OK;
 }
 
@@ -104,6 +127,7 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   size_t o_prog = put(blob, f.prog), o_lights = put(blob, f.lights), o_tex = put(blob, f.textures);
   size_t o_texels = put(blob, f.texels);
   RT_HIP(hipSetDevice(c->device));
+  RT_TRY(rt::wait_launches(c));       // launches in flight read the blob and may run the specialised modules
   if (c->d_blob) { (void)hipFree(c->d_blob); c->d_blob = nullptr; }
   c->uploaded = false;
   RT_HIP(hipMalloc(&c->d_blob, blob.size()));
@@ -122,7 +146,6 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   d.lights = (const RtLight*)(b + o_lights);
   d.textures = (const RtTexture*)(b + o_tex);
   d.texels = b + o_texels;
-  c->tbl_bytes = o_texels - o_obj;
   d.n_objects = (int32_t)f.objects.size();
   d.n_lights = (int32_t)f.lights.size();
   d.n_leaves = (int32_t)f.leaves.size();
@@ -150,34 +173,51 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   }
   c->uploaded = true;
   drop_orders(c);                     // tile costs belong to the previous scene
-  // the scene-specialised program (spec.hip): the row kernels of the scene's mode; reflection-only
-  // scenes also get the deferred kernels (their tail-bound launches' choice)
-  rt::spec_drop(c);
-  c->spec_flat = std::make_shared<rt::FlatScene>(f);
+  // the scene-specialised programs (spec.hip): requested from the compile pool, loaded by the first
+  // launch after they are ready; the generic kernels render until then.  Only the flags are computed
+  // here -- the program text (and a family lookup) only when the option is on and the scene fits.
+  rt::spec_drop(c);                   // the previous scene's modules (the hipFree above waited for the device)
+  c->spec_flat = std::make_shared<rt::FlatScene>(std::move(f));
   c->spec_flat->texels.clear();
   c->spec_flat->texels.shrink_to_fit();
-  rt::spec_program(*c->spec_flat, c);
-  if (c->spec_on) {
-    int rc = rt::spec_build(c);
-    if (rc) return rc;
-  }
+  rt::spec_flags(*c->spec_flat, c);
+  rt::spec_prepare(c);
   return RT_OK;
 }
 
 int rt_ctx_kernel_info(rt_ctx* c, char* buf, size_t cap) {
   if (!c || !buf || cap == 0) return fail(RT_ERR_INVALID, "null argument");
-  char s[640];
-  if (c->spec_mod)
-    snprintf(s, sizeof s, "scene-specialised (hipRTC %016llx, %s%s, compiled in %.0f ms%s by %s); last launch: %s",
-             (unsigned long long)c->spec_hash, c->spec_mode == RT_MODE_REFL ? "reflection" : c->spec_mode == RT_MODE_CHAIN ? "chain" : "tree",
+  std::string s;
+  char b[1024];
+  if (c->spec_mod) {
+    snprintf(b, sizeof b, "scene-specialised (hipRTC %016llx, %s%s, compiled in %.0f ms%s by %s; %s; loaded %.0f ms after "
+             "the request)", (unsigned long long)c->spec_hash,
+             c->spec_mode == RT_MODE_REFL ? "reflection" : c->spec_mode == RT_MODE_CHAIN ? "chain" : "tree",
              c->spec_family ? (", family of " + std::to_string(c->spec_family) + " scenes").c_str() : "",
-             c->spec_compile_ms, c->spec_compile_ms == 0.0 ? " [process cache]" : "", rt::spec_compiler(), c->last_kernel);
-  else if (c->spec_on && c->uploaded && !c->spec_fits)
-    snprintf(s, sizeof s, "generic (librt_mi355x.so; scene too large to specialise: > %d objects or > %d leaves); last "
-             "launch: %s", RT_SPEC_MAX_OBJECTS, RT_SPEC_MAX_LEAVES, c->last_kernel);
-  else
-    snprintf(s, sizeof s, "generic (librt_mi355x.so); last launch: %s", c->last_kernel);
-  snprintf(buf, cap, "%s", s);
+             c->spec_compile_ms, c->spec_note.c_str(), rt::spec_compiler(), c->spec_res.c_str(), c->spec_ready_ms);
+    s = b;
+  } else if (c->spec_on && c->uploaded && !c->spec_fits) {
+    snprintf(b, sizeof b, "generic (librt_mi355x.so; scene too large to specialise: > %d objects or > %d leaves)",
+             RT_SPEC_MAX_OBJECTS, RT_SPEC_MAX_LEAVES);
+    s = b;
+  } else if (c->spec_on && c->uploaded && !c->spec_jobs.empty()) {
+    s = "generic (librt_mi355x.so; the scene-specialised program is compiling in the background)";
+  } else if (c->spec_on && c->uploaded && !c->spec_error.empty()) {
+    s = "generic (librt_mi355x.so; specialisation failed: " + c->spec_error + ")";
+  } else {
+    s = "generic (librt_mi355x.so)";
+  }
+  s += std::string("; last launch: ") + c->last_kernel;
+  snprintf(buf, cap, "%s", s.c_str());
+  return RT_OK;
+}
+
+int rt_ctx_spec_wait(rt_ctx* c, int32_t timeout_ms) {
+  if (!c) return fail(RT_ERR_INVALID, "null context");
+  RT_HIP(hipSetDevice(c->device));
+  const int rc = rt::spec_wait(c, (double)timeout_ms);
+  if (rc == RT_PENDING) return RT_PENDING;
+  if (!c->spec_error.empty()) return fail(RT_ERR_UNSUPPORTED, "%s", c->spec_error.c_str());
   return RT_OK;
 }
 
@@ -197,25 +237,22 @@ int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
     c->timed = false;                  // no launch recorded under the new setting yet
     return RT_OK;
   }
-  if (option == RT_OPT_TAIL_TILES) {
-    if (value < 0 || value > 4096) return fail(RT_ERR_INVALID, "RT_OPT_TAIL_TILES %d not in [0, 4096]", value);
-    if (value != c->tail_tiles) {
-      RT_HIP(hipSetDevice(c->device));
-      drop_orders(c);                            // the tail set is chosen at calibration
-      c->tail_tiles = value;
-    }
-    return RT_OK;
-  }
   if (option == RT_OPT_SPECIALIZE) {
     if (value < 0 || value > 2) return fail(RT_ERR_INVALID, "RT_OPT_SPECIALIZE value %d", value);
-    if (value == c->spec_on) return RT_OK;
+    const bool retry = value == c->spec_on && !c->spec_error.empty();   // the same value again: compile again
+    if (value == c->spec_on && !retry) return RT_OK;
     RT_HIP(hipSetDevice(c->device));
-    RT_HIP(hipDeviceSynchronize());             // launches in flight may still run the modules
+    int rc = rt::wait_launches(c);              // this context's launches in flight may still run the modules
+    if (rc) return rc;
     rt::spec_drop(c);
     c->spec_on = value;
-    if (!c->uploaded || !value) return RT_OK;
-    rt::spec_program(*c->spec_flat, c);         // a scene family registered since the upload may hold it
-    return rt::spec_build(c);
+    if (c->uploaded) rt::spec_prepare(c, retry);   // a scene family registered since the upload may hold it
+    return RT_OK;
+  }
+  if (option == RT_OPT_TILES_PER_WAVE) {
+    if (value < 0 || value > 16) return fail(RT_ERR_INVALID, "RT_OPT_TILES_PER_WAVE %d not in [0, 16]", value);
+    c->tiles_per_wave = value;
+    return RT_OK;
   }
   if (option == RT_OPT_WAVEFRONT_PAIRS) {
     if (value < 0 || value > 2) return fail(RT_ERR_INVALID, "RT_OPT_WAVEFRONT_PAIRS %d not in [0, 2]", value);
@@ -276,16 +313,18 @@ int rt_stream_destroy(void* stream) {
 int rt_ctx_synchronize(rt_ctx* c) {
   if (!c) return fail(RT_ERR_INVALID, "null context");
   RT_HIP(hipSetDevice(c->device));
-  RT_HIP(hipStreamSynchronize(c->stream));
-  return RT_OK;
+  return rt::wait_launches(c);
 }
 
 void rt_ctx_free(rt_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  // the whole device, not c->stream: the caller's last stream may be destroyed by now (bench.py's
-  // frames-in-flight streams are; synchronising a destroyed stream crashed at exit in round 4)
-  (void)hipDeviceSynchronize();
+  // this context's own launches, through its completion events: not the device (other contexts'
+  // work), not a caller's stream (bench.py's frames-in-flight streams are destroyed by now;
+  // synchronising a destroyed stream crashed at exit in round 4)
+  (void)rt::wait_launches(c);
+  for (auto& m : c->marks) (void)hipEventDestroy(m.ev);
+  c->marks.clear();
   if (c->d_blob) (void)hipFree(c->d_blob);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->wf) (void)hipFree(c->wf);
@@ -293,9 +332,6 @@ void rt_ctx_free(rt_ctx* c) {
   if (c->wfp) (void)hipFree(c->wfp);
   drop_orders(c);
   rt::spec_drop(c);
-  if (c->tail_stream) (void)hipStreamDestroy(c->tail_stream);
-  if (c->tail_ev0) (void)hipEventDestroy(c->tail_ev0);
-  if (c->tail_ev1) (void)hipEventDestroy(c->tail_ev1);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->tev0) (void)hipEventDestroy(c->tev0);

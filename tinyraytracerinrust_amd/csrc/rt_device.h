@@ -116,9 +116,8 @@ namespace {
 
 // Scene tables are read-only for the whole launch: view them through the CONSTANT address space
 // (4) so uniform-index reads compile to scalar (SMEM) loads instead of per-lane VMEM loads.
-// RT_CAS_GENERIC (k_tail.hip): the tables are read through generic (flat) pointers instead -- the tail
-// kernel stages them in LDS, where lanes read different records at LDS latency.
-#if defined(RT_CAS_GENERIC) || defined(RT_SPEC_FAMILY)
+// A family program (RT_SPEC_FAMILY) reads its tables through generic pointers (fam_rec).
+#if defined(RT_SPEC_FAMILY)
 #define CAS
 #else
 #define CAS __attribute__((address_space(4)))
@@ -696,84 +695,6 @@ RT_FN double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
   return done ? 0.0 : tr;
 }
 
-// ---------------------------------------------------------------- cooperative walks (the tail kernel)
-// One ray per group of G lanes (G = 8 .. 64, groups aligned in the wave): lane j of a group takes the
-// leaves j, j + G, j + 2G, ... of the whole scene (RtLeaf::object names each leaf's object), runs the
-// same culls (its object's box and oriented box, the leaf's box -- against the whole segment, so
-// conservative) and the same leaf test and hit filter as nearest_hit, and the group reduces.  The
-// nearest hit is the least (distance, object) over every accepted candidate: exactly the reference's
-// first-visited-wins walk in draw order (raytracer.rs:141-150).  A lane's leaf reads are per-lane
-// (vector) loads; a lone costly pixel's walk then takes about one leaf test instead of all of them.
-template <int G>
-__device__ __forceinline__ void group_min(double* t, int* o) {
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) {
-    const double t2 = __shfl_xor(*t, m, G);
-    const int o2 = __shfl_xor(*o, m, G);
-    if (t2 < *t || (t2 == *t && o2 < *o)) { *t = t2; *o = o2; }
-  }
-}
-template <int G>
-RT_FN int nearest_hit_coop(const DS& S, int n_leaves, V3 ro, V3 rd, double* dist) {
-  const int j = (int)(__lane_id() & (G - 1));
-  const CullRay cr = cull_ray(ro, rd);
-  const bool fin = wave_finite(ro, rd);
-  double best = INFINITY;
-  int bobj = 0x7fffffff;
-  for (int l = j; l < n_leaves; l += G) {
-    cptr<RtLeaf> L = &S.leaves[l];
-    const int o = L->object;
-    cptr<RtObject> O = &S.objects[o];
-    if (O->cull == RT_CULL_ALWAYS) continue;
-    if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, cr, INFINITY)) continue;
-    if (RT_OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, ro, rd, INFINITY)) continue;
-    if (O->leaf_cull) {
-      if (L->cull == RT_CULL_ALWAYS) continue;
-      if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, INFINITY)) continue;
-    }
-    double t0 = 0.0, t1 = 0.0;
-    const int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1);
-    const bool filtered = L->prog_end != L->prog_begin;
-    if (n >= 1 && t0 > EPS && (t0 < best || (t0 == best && o < bobj)) &&
-        (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) { best = t0; bobj = o; }
-    if (n >= 2 && t1 > EPS && (t1 < best || (t1 == best && o < bobj)) &&
-        (!filtered || leaf_filter(S, L, add(ro, scale(rd, t1))))) { best = t1; bobj = o; }
-  }
-  group_min<G>(&best, &bobj);
-  *dist = best;
-  return best < INFINITY ? bobj : -1;
-}
-// Shadow rays of scenes whose every transparency is +-0 (no transparent object): the product is 0 at
-// the first filtered hit in (EPS, dist) and 1 without one (raytracer.rs:181-197), so the group ORs.
-template <int G>
-RT_FN double shadow_coop(const DS& S, int n_leaves, V3 p, V3 dir, double dist) {
-  const int j = (int)(__lane_id() & (G - 1));
-  const CullRay cr = cull_ray(p, dir);
-  const bool fin = wave_finite(p, dir);
-  const double tmax = cull_tmax(dist);
-  int hit = 0;
-  for (int l = j; l < n_leaves && !hit; l += G) {
-    cptr<RtLeaf> L = &S.leaves[l];
-    cptr<RtObject> O = &S.objects[L->object];
-    if (O->shadow_skip || O->cull == RT_CULL_ALWAYS) continue;
-    if (O->cull == RT_CULL_BOX && !box_may_hit(O->blo, O->bhi, cr, tmax)) continue;
-    if (RT_OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, p, dir, tmax)) continue;
-    if (O->leaf_cull) {
-      if (L->cull == RT_CULL_ALWAYS) continue;
-      if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
-    }
-    double t0 = 0.0, t1 = 0.0;
-    const int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1);
-    const bool filtered = L->prog_end != L->prog_begin;
-    if ((n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) ||
-        (n >= 2 && t1 > EPS && t1 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t1))))))
-      hit = 1;
-  }
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) hit |= __shfl_xor(hit, m, G);
-  return hit ? 0.0 : 1.0;
-}
-
 // Normal and UV of top-level object O at point p: RTObject shape get_normal / get_uv_coordinates,
 // with CSG's is_on_surface / is_inside evaluated bottom-up over the post-order node list
 // (csg.rs:98-168) and the descent a-then-b of csg.rs:104-121 / :161-167.
@@ -985,10 +906,8 @@ typedef LDS_AS double lds_f64;
 // KLR > 0 (REFR): the pending-reflection state of frames 0..KLR-1 at lf[(KL * 4 + f * 7 + c) * 64].
 // CHAIN (REFR scenes with RtDevScene::ray_chains): every hit spawns at most one ray, so a refraction
 // frame never carries a pending reflection: frames are (A, w) as in the reflection-only kernels.
-// COOP > 0 (reflection-only scenes, the tail kernel): G = COOP lanes trace one ray together
-// (nearest_hit_coop / shadow_coop); every lane of a group computes the same colour.
-template <bool REFR, class Rec = NoRec, int KL = 0, bool FC = false, int KLR = 0, bool CHAIN = false, int COOP = 0>
-RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, lds_f64* lf = nullptr, int n_leaves = 0) {
+template <bool REFR, class Rec = NoRec, int KL = 0, bool FC = false, int KLR = 0, bool CHAIN = false>
+RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, lds_f64* lf = nullptr) {
   double fA[RT_MAX_DEPTH_CAP][3];     // parent colour already intensified by (1 - w)
   double fW[RT_MAX_DEPTH_CAP];        // child weight w (transparency or reflectivity)
   auto put_frame = [&](int f, Col A, double w) {
@@ -1041,8 +960,7 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
     bool descend = false;
     double t_hit;
     int oi;
-    if constexpr (COOP > 0) oi = nearest_hit_coop<COOP>(S, n_leaves, ro, rd, &t_hit);
-    else oi = nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit);
+    oi = nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit);
     const V3 p = add(ro, scale(rd, t_hit));                               // :162
     if constexpr (RECORD) slot = rec->begin(depth, ray_type, ro, rd, t_hit, oi, p);
     V3 nrm = {0.0, 0.0, 0.0};
@@ -1065,8 +983,7 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
         len_inv(lv, &ll, &ill);
         const V3 sdir = scale(lv, ill);                                    // normalized(lv)
         double t;                                                          // :176-197
-        if constexpr (COOP > 0) t = shadow_coop<COOP>(S, n_leaves, p, sdir, ll);
-        else t = shadow_transparency<SHARE, OBB>(S, p, sdir, ll);
+        t = shadow_transparency<SHARE, OBB>(S, p, sdir, ll);
         if (!have_shading) {
           shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
           L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));                      // ambient (:172)
@@ -1436,16 +1353,19 @@ __device__ __forceinline__ void store_pixel(uint8_t* row, int x, Col c, int rgb)
 // on a calibration launch that stored each tile's wave time in `cost`.  CAL (the calibration
 // instantiation) is the only one that carries the timing code.
 // KL_ >= 0: that many stack frames in LDS (the specialised kernels at 4 waves/SIMD have room for more).
+// rows_entry: entry `entry` of the launch (a tile index, or the order's entry-th tile); rows_body: the
+// workgroup's own entry (blockIdx.x).  The specialised kernels may loop a wave over several entries
+// (spec.hip, RT_OPT_TILES_PER_WAVE: cheap launches whose waves are too short to amortise their dispatch).
 template <int MODE, bool F64, bool CAL, bool FC, int KL_ = -1>
-__device__ __forceinline__ void rows_body(const RtDevScene& S, int y_first, int band_rows, int band_pitch, int n_rows,
-                                          int max_depth, uint8_t* __restrict__ out, size_t stride,
-                                          const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb,
-                                          lds_f64* frames) {
+__device__ __forceinline__ void rows_entry(const RtDevScene& S, unsigned entry, int y_first, int band_rows, int band_pitch,
+                                           int n_rows, int max_depth, uint8_t* __restrict__ out, size_t stride,
+                                           const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb,
+                                           lds_f64* frames) {
   constexpr bool REFR = MODE != RT_MODE_REFL, CHAIN = MODE == RT_MODE_CHAIN;
   constexpr int KLR = MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0;
   constexpr int KL = KL_ >= 0 ? KL_ : CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES;
   const int lane = threadIdx.x & 63;
-  const unsigned tile = CAL || !order ? blockIdx.x : (unsigned)order[blockIdx.x];
+  const unsigned tile = CAL || !order ? entry : (unsigned)order[entry];
   [[maybe_unused]] uint64_t t_start = 0;
   if constexpr (CAL) t_start = wall_clock64();
   int x, r;
@@ -1459,6 +1379,14 @@ __device__ __forceinline__ void rows_body(const RtDevScene& S, int y_first, int 
   store_pixel<F64>(out + (size_t)r * stride, x, c, rgb);
   if constexpr (CAL)
     if (threadIdx.x == 0) cost[tile] = (uint32_t)(wall_clock64() - t_start);   // vector store
+}
+template <int MODE, bool F64, bool CAL, bool FC, int KL_ = -1>
+__device__ __forceinline__ void rows_body(const RtDevScene& S, int y_first, int band_rows, int band_pitch, int n_rows,
+                                          int max_depth, uint8_t* __restrict__ out, size_t stride,
+                                          const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb,
+                                          lds_f64* frames) {
+  rows_entry<MODE, F64, CAL, FC, KL_>(S, blockIdx.x, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, order,
+                                      cost, rgb, frames);
 }
 template <int MODE, int KL_ = -1>
 constexpr int rows_lds_doubles() {
@@ -1501,29 +1429,5 @@ __device__ __forceinline__ void deferred_body(const RtDevScene& S, int y_first, 
 #ifndef RT_WAVES_PER_EU_DEFERRED
 #define RT_WAVES_PER_EU_DEFERRED 7
 #endif
-
-// The tail kernel's body (reflection-only scenes): the costliest tiles of a tail-bound ordered launch,
-// taken out of the main launch (launch_bands) and traced G lanes per pixel (trace<..., COOP = G>), so
-// a lone costly pixel's chain waits for one leaf test per walk instead of the whole walk.  Wave w
-// renders pixels [part * 64/G, (part + 1) * 64/G) of tile tiles[w / G], part = w % G.
-template <bool F64, bool FC, int G>
-__device__ __forceinline__ void tail_body(const RtDevScene& S, int y_first, int band_rows, int band_pitch, int n_rows,
-                                          int max_depth, uint8_t* __restrict__ out, size_t stride,
-                                          const int32_t* __restrict__ tiles, int rgb, lds_f64* frames) {
-  constexpr int PPW = 64 / G;
-  const int lane = threadIdx.x & 63;
-  const unsigned tile = (unsigned)tiles[blockIdx.x / G];
-  const int pix = (int)(blockIdx.x % G) * PPW + lane / G;
-  int x, r;
-  tile_pixel(tile, pix, S.width, &x, &r);
-  if (x >= S.width || r >= n_rows) return;                         // the whole group: same pixel
-  const int y = y_first + (r / band_rows) * band_pitch + r % band_rows;
-  if (y >= S.height) return;
-  V3 ro, rd;
-  camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
-  const Col c = trace<false, NoRec, RT_LDS_FRAMES, FC, 0, false, G>(make_ds(S), ro, rd, max_depth, nullptr, frames + lane,
-                                                                    S.n_leaves);
-  if ((lane & (G - 1)) == 0) store_pixel<F64>(out + (size_t)r * stride, x, c, rgb);
-}
 
 }  // namespace

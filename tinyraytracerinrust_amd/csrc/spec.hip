@@ -1,4 +1,4 @@
-// spec.hip -- scene-specialised row kernels (rt_ctx_set_option(RT_OPT_SPECIALIZE, 1)).
+// spec.hip -- scene-specialised row kernels (rt_ctx_set_option(RT_OPT_SPECIALIZE), default on).
 //
 // The generic kernels read the flattened scene (rt_blob.h) from HBM: every hierarchy step, object
 // and leaf record is a dependent scalar load, and every branch on a record field (leaf kind,
@@ -9,17 +9,32 @@
 // values is unchanged -- the same operations in the same order, -ffp-contract=off, constant folding
 // only of values the host computed already -- so the pixels are bit-identical (tests/test_gpu_spec.py).
 //
-// hipRTC (libhiprtc, ROCm) compiles the program at scene upload; the code object is cached per
-// process by the program text's hash, and loaded as a module on the context's device.  Launches
-// take a specialised kernel when one matches (k_rows.hip), the generic one otherwise.
+// Life of a program (round 5):
+//   * rt_ctx_upload REQUESTS the scene's programs and returns at once: a small pool of library
+//     threads compiles them with hipRTC (or finds them in the process cache / the on-disk cache),
+//     while the context renders with the generic kernels;
+//   * the first launch after the compile finished loads the code objects on the context's device and
+//     every later launch takes them (k_rows.hip launch_bands -> spec_poll); rt_ctx_spec_wait blocks
+//     for them (hosts that want the specialised kernels from their first timed frame, and tests);
+//   * a program is keyed by its FULL text (the process cache compares the text, the disk cache the
+//     text and the compiler's identity), never by a hash alone;
+//   * guards: only the ROCm installation's hipRTC compiles (loaded into a link-map namespace of its
+//     own, see rtc()), and a code object whose resource use exceeds the known-good bound (VGPRs,
+//     scratch per lane, from the code object's metadata) is refused -- the context then keeps
+//     the generic kernels and rt_ctx_kernel_info says why.  A failed compile never fails an upload.
 #include <dlfcn.h>
 #include <hip/hiprtc.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -51,6 +66,8 @@ struct Rtc {
   const char* (*err)(hiprtcResult);
   hiprtcResult (*version)(int*, int*);
   std::string origin;                  // which hipRTC: the kernel info's "compiler" note
+  bool rocm = false;                   // the ROCm installation's own (the only one the guard lets compile)
+  std::string identity;                // origin + the library file's real path, size and mtime (disk-cache key)
 };
 const Rtc& rtc() {
   static const Rtc r = [] {
@@ -70,6 +87,7 @@ const Rtc& rtc() {
       x.err = (decltype(x.err))sym("hiprtcGetErrorString");
       x.version = (decltype(x.version))sym("hiprtcVersion");
       x.origin = path;
+      x.rocm = true;
     } else {
       x.create = hiprtcCreateProgram;
       x.compile = hiprtcCompileProgram;
@@ -84,23 +102,24 @@ const Rtc& rtc() {
     }
     int ma = 0, mi = 0;
     if (x.version && x.version(&ma, &mi) == HIPRTC_SUCCESS) x.origin += " " + std::to_string(ma) + "." + std::to_string(mi);
+    x.identity = x.origin;
+    if (char* rp = realpath(path.c_str(), nullptr)) {
+      struct stat st;
+      if (stat(rp, &st) == 0)
+        x.identity += std::string(" ") + rp + " " + std::to_string((long long)st.st_size) + " " + std::to_string((long long)st.st_mtime);
+      free(rp);
+    }
     return x;
   }();
   return r;
 }
-
-struct SpecCode {
-  std::vector<char> code;              // the linked code object
-  double compile_ms = 0.0;
-};
-std::mutex g_spec_mu;
-std::map<uint64_t, std::shared_ptr<SpecCode>> g_spec_cache;
 
 uint64_t fnv1a(const std::string& s) {
   uint64_t h = 1469598103934665603ull;
   for (unsigned char ch : s) { h ^= ch; h *= 1099511628211ull; }
   return h;
 }
+std::mutex g_spec_mu;                  // the job table and the registered families
 
 // constexpr T NAME[] = { bit_cast<T>(words), ... }: the host record's exact bits (padding included).
 // vary (a family program): per 4-byte word, 1 = the word differs between the family's members -- it is
@@ -182,8 +201,10 @@ struct SpecFamily {
   rt::FlatScene base;                  // member 0, without its texels
   std::vector<uint8_t> v_obj, v_trav, v_strav, v_leaf, v_light;
   std::string src;                     // the program's prelude
+  std::vector<std::shared_ptr<rt::SpecJob>> jobs;   // its compiled kernels, kept resident while registered
 };
 std::vector<std::shared_ptr<SpecFamily>> g_families;   // under g_spec_mu; newest last
+std::vector<std::shared_ptr<SpecFamily>> g_singles;    // "families" of one registered scene: hold its own program
 
 // Same structure: equal table sizes, flags, hierarchy nodes, CSG nodes, filter programs and
 // texture records (the family program holds those as plain constants).
@@ -204,12 +225,32 @@ bool family_member(const SpecFamily& F, const rt::FlatScene& f) {
 
 namespace rt {
 
+// A diagnostic build's -D switches (Makefile: $(DIAG) as the string RT_SPEC_DIAG_DEFINES) as #define
+// lines for the programs' prelude, so the specialised kernels of a diagnostic build are built the way
+// its precompiled kernels are (empty in the product build).
+#ifndef RT_SPEC_DIAG_DEFINES
+#define RT_SPEC_DIAG_DEFINES ""
+#endif
+static std::string diag_prelude() {
+  std::string out, w;
+  const std::string s = RT_SPEC_DIAG_DEFINES;
+  for (size_t i = 0; i <= s.size(); ++i) {
+    if (i < s.size() && s[i] != ' ') { w += s[i]; continue; }
+    if (w.rfind("-D", 0) == 0 && w.size() > 2) {
+      const size_t eq = w.find('=');
+      out += "#define " + (eq == std::string::npos ? w.substr(2) : w.substr(2, eq - 2) + " " + w.substr(eq + 1)) + "\n";
+    }
+    w.clear();
+  }
+  return out;
+}
+
 // The program's prelude: the scene's tables as constexpr data, then the device code.  fam: the
 // family's program (the words that differ between members zeroed, their masks emitted).
 static std::string spec_source(const FlatScene& f, const SpecFamily* fam) {
   std::string s;
   char buf[256];
-  s += std::string("// scene-specialised row kernels (spec.hip)\n#define RT_SPEC 1\n") +
+  s += std::string("// scene-specialised row kernels (spec.hip)\n#define RT_SPEC 1\n") + diag_prelude() +
        (fam ? "#define RT_SPEC_FAMILY 1\n" : "") + "#define RT_TILE_W " + std::to_string(RT_TILE_W) +
        "\n#include \"rt_blob.h\"\n";
   s += "template <int N> struct SpecRaw { unsigned long long w[N]; };\nnamespace rt_spec {\n";
@@ -251,13 +292,18 @@ static std::string spec_kernel(int kind, int mode, bool fc, int f64, int cal) {
 #else
   const int kl = -1;
 #endif
+  // the megakernel takes its entries grid-stride: entry blockIdx.x, + gridDim.x, ... < n_entries (launch_bands
+  // launches n_entries / tiles-per-wave workgroups for cheap launches; one entry per wave otherwise)
   if (kind == 0)
     snprintf(buf, sizeof buf,
              "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(%s))) "
-             "void rt_spec_rows_%d%d%s {\n  __shared__ double s_frames[rows_lds_doubles<%d, %d>()];\n"
-             "  rows_body<%d, %s, %s, %s, %d>(S, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, order, "
+             "void rt_spec_rows_%d%d(RtDevScene S, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth, "
+             "uint8_t* __restrict__ out, size_t stride, const int32_t* __restrict__ order, uint32_t* __restrict__ cost, "
+             "int rgb, unsigned n_entries) {\n  __shared__ double s_frames[rows_lds_doubles<%d, %d>()];\n"
+             "  for (unsigned e = blockIdx.x; e < n_entries; e += gridDim.x)\n"
+             "    rows_entry<%d, %s, %s, %s, %d>(S, e, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, order, "
              "cost, rgb, (lds_f64*)s_frames);\n}\n",
-             waves, f64, cal, args, mode, kl, mode, f64 ? "true" : "false", cal ? "true" : "false", fc ? "true" : "false", kl);
+             waves, f64, cal, mode, kl, mode, f64 ? "true" : "false", cal ? "true" : "false", fc ? "true" : "false", kl);
   else
     snprintf(buf, sizeof buf,
              "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_DEFERRED))) "
@@ -289,58 +335,201 @@ static std::vector<std::string> spec_programs(const rt_ctx* c) {
   return v;
 }
 
-const char* spec_compiler() { return rtc().origin.c_str(); }
+// ---- programs: the job table and the compile pool -------------------------------------------------
+enum { SPEC_QUEUED = 0, SPEC_RUNNING, SPEC_DONE, SPEC_FAILED, SPEC_CANCELLED };
 
-void spec_drop(rt_ctx* c) {
-  for (auto& m : c->spec_mods)
-    if (m) (void)hipModuleUnload(m);
-  memset(c->spec_mods, 0, sizeof c->spec_mods);
-  c->spec_mod = nullptr;
-  memset(c->spec_rows, 0, sizeof c->spec_rows);
-  memset(c->spec_def, 0, sizeof c->spec_def);
+struct SpecCode {
+  std::vector<char> code;              // the linked code object
+  std::string name;                    // the kernel (code-object metadata .name)
+  double compile_ms = 0.0;             // the hipRTC compile that made it (0: read from the disk cache)
+  bool from_disk = false;
+  int vgprs = -1, sgprs = -1, scratch = -1, vspill = -1, occupancy = -1;   // code-object metadata (occupancy: VGPR-limited)
+};
+
+// One program (prelude + one kernel), keyed by its full text.  `interest` counts the holders (contexts,
+// registered families, callers waiting for it): a job nobody holds when a worker reaches it is
+// cancelled, so a host that uploads scene after scene (the reference's animate mode builds every
+// frame's scene anew, gui.rs:78-89) only ever compiles what it still renders.
+struct SpecJob {
+  std::string text;
+  std::atomic<int> state{SPEC_QUEUED};
+  std::atomic<int> interest{0};
+  SpecCode code;                       // valid once SPEC_DONE
+  std::string error;                   // set once SPEC_FAILED
+  uint64_t last_use = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+};
+
+}  // namespace rt
+
+namespace {
+
+using rt::SpecCode;
+using rt::SpecJob;
+using rt::SPEC_QUEUED;
+using rt::SPEC_RUNNING;
+using rt::SPEC_DONE;
+using rt::SPEC_FAILED;
+using rt::SPEC_CANCELLED;
+
+// At most this many compiles at once (hipRTC / LLVM: seconds and hundreds of MB each).
+constexpr size_t RT_SPEC_WORKERS_MAX = 4;
+// Completed programs the process keeps when nobody holds them (LRU beyond this many jobs).
+constexpr size_t RT_SPEC_CACHE_JOBS = 64;
+// Resource guard: the known-good bounds of the specialised kernels (ROCm 7.2's LLVM: the reflection and
+// chain megakernels at most 128 VGPRs at 4 waves/SIMD with 528-576 B/lane of scratch; the ray-tree
+// megakernel 1 424 B/lane for its pending-reflection stack, the deferred kernel 1 568 B/lane for its
+// per-lane hit records).  PyTorch's bundled LLVM 20 built the chain family megakernel with 1.4 KB/lane
+// and ran it 19x slower (profiles/r05v_family_compilers.txt): that is what the guard refuses.
+#ifndef RT_SPEC_MAX_VGPRS
+#define RT_SPEC_MAX_VGPRS 128
+#endif
+#ifndef RT_SPEC_MAX_SCRATCH_ROWS
+#define RT_SPEC_MAX_SCRATCH_ROWS 1024
+#endif
+#ifndef RT_SPEC_MAX_SCRATCH_DEF
+#define RT_SPEC_MAX_SCRATCH_DEF 2048
+#endif
+#ifndef RT_SPEC_MAX_SCRATCH_TREE
+#define RT_SPEC_MAX_SCRATCH_TREE 2048
+#endif
+
+struct SpecState {                     // under g_spec_mu; never destroyed (workers may outlive exit's destructors)
+  std::map<std::string, std::shared_ptr<SpecJob>> jobs;   // by full program text
+  uint64_t clock = 0;
+  std::deque<std::shared_ptr<SpecJob>> queue;
+  std::vector<std::thread> workers;
+  std::condition_variable qcv;
+  bool stop = false;
+  std::string disk_dir;                // rt_spec_cache_dir: "" = no on-disk cache
+};
+SpecState& sst() {
+  static SpecState* p = new SpecState;
+  return *p;
+}
+
+void job_finish(SpecJob* j, int state) {
+  {
+    std::lock_guard<std::mutex> lk(j->mu);
+    j->state = state;
+  }
+  j->cv.notify_all();
+}
+
+// A token of interest in job j: a shared_ptr to the job whose deleter drops the interest again.
+std::shared_ptr<SpecJob> job_token(const std::shared_ptr<SpecJob>& j) {
+  j->interest++;
+  return std::shared_ptr<SpecJob>(j.get(), [j](SpecJob*) { j->interest--; });
+}
+
+bool job_finished(const SpecJob* j) {
+  const int s = j->state.load();
+  return s == SPEC_DONE || s == SPEC_FAILED || s == SPEC_CANCELLED;
+}
+
+// Waits for j (timeout_ms < 0: no limit); true once it has finished.
+bool job_wait(SpecJob* j, double timeout_ms) {
+  std::unique_lock<std::mutex> lk(j->mu);
+  if (timeout_ms < 0) {
+    j->cv.wait(lk, [&] { return job_finished(j); });
+    return true;
+  }
+  return j->cv.wait_for(lk, std::chrono::duration<double, std::milli>(timeout_ms), [&] { return job_finished(j); });
+}
+
+// The kernel's resource use from the code object's AMDGPU metadata note (msgpack): the map entry after
+// the key string, e.g. ".vgpr_count" -> 128.  One kernel per program, so every key occurs once.
+// (hipRTC's -Rpass-analysis=kernel-resource-usage remarks say the same, but emitting them crashed the
+// compiler inside its own link-map namespace.)
+bool mp_value(const std::vector<char>& b, const char* key, long long* ival, std::string* sval) {
+  const size_t n = strlen(key);
+  std::string pat;
+  if (n < 32) pat += (char)(0xa0 | n);
+  else { pat += (char)0xd9; pat += (char)n; }
+  pat += key;
+  const auto it = std::search(b.begin(), b.end(), pat.begin(), pat.end());
+  if (it == b.end()) return false;
+  size_t i = (size_t)(it - b.begin()) + pat.size();
+  if (i >= b.size()) return false;
+  const unsigned char t = (unsigned char)b[i];
+  auto be = [&](int bytes) {
+    unsigned long long v = 0;
+    for (int k = 1; k <= bytes && i + k < b.size(); ++k) v = v << 8 | (unsigned char)b[i + k];
+    return v;
+  };
+  if (sval) {
+    size_t len = 0, at = 0;
+    if ((t & 0xe0) == 0xa0) { len = t & 0x1f; at = i + 1; }
+    else if (t == 0xd9) { len = (size_t)be(1); at = i + 2; }
+    else return false;
+    if (at + len > b.size()) return false;
+    sval->assign(b.data() + at, len);
+    return true;
+  }
+  if (t <= 0x7f) *ival = t;
+  else if (t == 0xcc) *ival = (long long)be(1);
+  else if (t == 0xcd) *ival = (long long)be(2);
+  else if (t == 0xce) *ival = (long long)be(4);
+  else if (t == 0xcf) *ival = (long long)be(8);
+  else return false;
+  return true;
+}
+void code_resources(SpecCode* c) {
+  long long v = -1;
+  c->vgprs = mp_value(c->code, ".vgpr_count", &v, nullptr) ? (int)v : -1;
+  c->sgprs = mp_value(c->code, ".sgpr_count", &v, nullptr) ? (int)v : -1;
+  c->scratch = mp_value(c->code, ".private_segment_fixed_size", &v, nullptr) ? (int)v : -1;
+  c->vspill = mp_value(c->code, ".vgpr_spill_count", &v, nullptr) ? (int)v : -1;
+  c->occupancy = c->vgprs > 0 ? std::min(8, 512 / ((c->vgprs + 7) / 8 * 8)) : -1;   // VGPR-limited waves/SIMD
+  std::string name;
+  c->name = mp_value(c->code, ".name", nullptr, &name) ? name : "";
 }
 
 // hipRTC: the program (with the device headers as named headers), the flags the library's own
-// kernels are built with (Makefile HIPFLAGS: -O3, no contraction, no fast-math, MachineLICM off).
-static int spec_compile(const std::string& src, SpecCode* out) {
+// kernels are built with (Makefile HIPFLAGS: -O3, no contraction, no fast-math, MachineLICM off), and
+// the resource use the guard reads from the code object.
+int spec_compile(const std::string& src, SpecCode* out, std::string* err) {
   const char* headers[] = {spec_hdr_rt_device, spec_hdr_rt_blob, spec_hdr_rt_math};
   const char* names[] = {"rt_device.h", "rt_blob.h", "rt_math.h"};
   hiprtcProgram prog;
   const Rtc& R = rtc();
-  if (R.create(&prog, src.c_str(), "rt_spec.hip", 3, headers, names) != HIPRTC_SUCCESS)
-    return fail(RT_ERR_DEVICE, "hiprtcCreateProgram failed");
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                        "-mllvm", "-disable-machine-licm"};
-  const auto t0 = std::chrono::steady_clock::now();
+  if (R.create(&prog, src.c_str(), "rt_spec.hip", 3, headers, names) != HIPRTC_SUCCESS) {
+    *err = "hiprtcCreateProgram failed";
+    return RT_ERR_DEVICE;
+  }
+  std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                                   "-mllvm", "-disable-machine-licm"};
 #ifdef RT_DIAG_ENV
   // diagnostic builds: RT_SPEC_OPTS appends options (space-separated) for compiler A/B runs
   std::vector<std::string> extra;
-  std::vector<const char*> all(opts, opts + sizeof opts / sizeof opts[0]);
   if (const char* e = getenv("RT_SPEC_OPTS")) {
     std::string s(e), w;
     for (size_t i = 0; i <= s.size(); ++i)
       if (i == s.size() || s[i] == ' ') { if (!w.empty()) extra.push_back(w); w.clear(); } else w += s[i];
   }
-  for (const std::string& x : extra) all.push_back(x.c_str());
-  const hiprtcResult r = R.compile(prog, (int)all.size(), all.data());
-#else
-  const hiprtcResult r = R.compile(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+  for (const std::string& x : extra) opts.push_back(x.c_str());
 #endif
+  const auto t0 = std::chrono::steady_clock::now();
+  const hiprtcResult r = R.compile(prog, (int)opts.size(), opts.data());
   out->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  if (r != HIPRTC_SUCCESS) {
-    size_t n = 0;
-    R.log_size(prog, &n);
-    std::string log(n + 1, '\0');
-    R.log(prog, &log[0]);
-    R.destroy(&prog);
-    return fail(RT_ERR_DEVICE, "hipRTC compile of the specialised kernels failed: %s\n%.2000s", R.err(r),
-                log.c_str());
-  }
   size_t n = 0;
+  R.log_size(prog, &n);
+  std::string log(n + 1, '\0');
+  if (n) R.log(prog, &log[0]);
+  if (r != HIPRTC_SUCCESS) {
+    R.destroy(&prog);
+    char buf[2300];
+    snprintf(buf, sizeof buf, "hipRTC compile of the specialised kernels failed: %s\n%.2000s", R.err(r), log.c_str());
+    *err = buf;
+    return RT_ERR_DEVICE;
+  }
+  n = 0;
   R.code_size(prog, &n);
   out->code.resize(n);
   R.code(prog, out->code.data());
   R.destroy(&prog);
+  code_resources(out);
 #ifdef RT_DIAG_ENV
   if (const char* dir = getenv("RT_SPEC_DUMP_DIR")) {     // diagnostic builds: the code object and its text
     char path[512];
@@ -353,56 +542,199 @@ static int spec_compile(const std::string& src, SpecCode* out) {
   return RT_OK;
 }
 
-// The code objects of programs: from the process cache, else compiled in parallel (one thread per
-// program; hipRTC is thread-safe) and cached.  *compile_ms = the longest compile (0: all cached).
-static int spec_codes(const std::vector<std::string>& srcs, std::vector<std::shared_ptr<SpecCode>>* out,
-                      double* compile_ms) {
-  out->assign(srcs.size(), nullptr);
-  std::vector<uint64_t> h(srcs.size());
-  {
-    std::lock_guard<std::mutex> lk(g_spec_mu);
-    for (size_t i = 0; i < srcs.size(); ++i) {
-      h[i] = fnv1a(srcs[i]);
-      auto it = g_spec_cache.find(h[i]);
-      if (it != g_spec_cache.end()) (*out)[i] = it->second;
-    }
+int spec_guard(const SpecCode& c, const std::string& text, std::string* err) {
+  const bool def = c.name.rfind("rt_spec_def_", 0) == 0;
+  const bool tree = text.find("rows_entry<" + std::to_string(RT_MODE_TREE) + ",") != std::string::npos;
+  const int max_scratch = def ? RT_SPEC_MAX_SCRATCH_DEF : tree ? RT_SPEC_MAX_SCRATCH_TREE : RT_SPEC_MAX_SCRATCH_ROWS;
+  if (c.name.empty() || c.vgprs < 0 || c.scratch < 0) {
+    *err = "resource guard: the code object's metadata holds no resource usage for the kernel";
+    return RT_ERR_UNSUPPORTED;
   }
-  std::vector<std::shared_ptr<SpecCode>> fresh(srcs.size());
-  std::vector<int> rc(srcs.size(), RT_OK);
-  std::vector<std::string> err(srcs.size());
-  std::vector<std::thread> th;
-  for (size_t i = 0; i < srcs.size(); ++i) {
-    if ((*out)[i]) continue;
-    fresh[i] = std::make_shared<SpecCode>();
-    th.emplace_back([&, i] {
-      rc[i] = spec_compile(srcs[i], fresh[i].get());
-      if (rc[i]) err[i] = rt_last_error();      // the thread's own error slot
-    });
-  }
-  for (auto& x : th) x.join();
-  *compile_ms = 0.0;
-  for (size_t i = 0; i < srcs.size(); ++i)
-    if (rc[i]) return fail(rc[i], "%s", err[i].c_str());
-  std::lock_guard<std::mutex> lk(g_spec_mu);
-  for (size_t i = 0; i < srcs.size(); ++i) {
-    if ((*out)[i]) continue;
-    *compile_ms = std::max(*compile_ms, fresh[i]->compile_ms);
-    (*out)[i] = g_spec_cache.emplace(h[i], fresh[i]).first->second;
+  if (c.vgprs > RT_SPEC_MAX_VGPRS || c.scratch > max_scratch) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "resource guard: %s uses %d VGPRs and %d B/lane of scratch (bounds %d / %d)", c.name.c_str(),
+             c.vgprs, c.scratch, RT_SPEC_MAX_VGPRS, max_scratch);
+    *err = buf;
+    return RT_ERR_UNSUPPORTED;
   }
   return RT_OK;
 }
 
-void spec_program(const FlatScene& f, rt_ctx* c) {
+// On-disk cache entry: "RTSPEC02\n", then length-prefixed (u64) compiler identity, program text, kernel
+// name and code object, and the five resource numbers (i32).  A hit must match identity AND text.
+void put_blob(std::string& f, const void* p, uint64_t n) {
+  f.append((const char*)&n, 8);
+  f.append((const char*)p, n);
+}
+bool get_blob(const std::vector<char>& f, size_t* at, std::string* s) {
+  uint64_t n = 0;
+  if (*at + 8 > f.size()) return false;
+  memcpy(&n, f.data() + *at, 8);
+  *at += 8;
+  if (n > f.size() - *at) return false;
+  s->assign(f.data() + *at, n);
+  *at += n;
+  return true;
+}
+std::string disk_path(const std::string& dir, const std::string& identity, const std::string& text) {
+  char buf[64];
+  snprintf(buf, sizeof buf, "/spec_%016llx.rtco", (unsigned long long)fnv1a(identity + '\0' + text));
+  return dir + buf;
+}
+bool disk_read(const std::string& path, const std::string& identity, const std::string& text, SpecCode* out) {
+  FILE* fi = fopen(path.c_str(), "rb");
+  if (!fi) return false;
+  std::vector<char> f;
+  char buf[1 << 16];
+  size_t n;
+  while ((n = fread(buf, 1, sizeof buf, fi)) > 0) f.insert(f.end(), buf, buf + n);
+  fclose(fi);
+  static const char magic[] = "RTSPEC02\n";
+  if (f.size() < 9 || memcmp(f.data(), magic, 9) != 0) return false;
+  size_t at = 9;
+  std::string id, tx, name, code;
+  if (!get_blob(f, &at, &id) || id != identity || !get_blob(f, &at, &tx) || tx != text || !get_blob(f, &at, &name) ||
+      !get_blob(f, &at, &code) || at + 20 > f.size())
+    return false;
+  int v[5];
+  memcpy(v, f.data() + at, 20);
+  out->name = name;
+  out->code.assign(code.begin(), code.end());
+  out->vgprs = v[0]; out->sgprs = v[1]; out->scratch = v[2]; out->vspill = v[3]; out->occupancy = v[4];
+  out->compile_ms = 0.0;
+  out->from_disk = true;
+  return true;
+}
+void disk_write(const std::string& dir, const std::string& path, const std::string& identity, const std::string& text,
+                const SpecCode& c) {
+  for (size_t i = 1; i <= dir.size(); ++i)              // mkdir -p
+    if (i == dir.size() || dir[i] == '/') (void)mkdir(dir.substr(0, i).c_str(), 0755);
+  std::string f("RTSPEC02\n");
+  put_blob(f, identity.data(), identity.size());
+  put_blob(f, text.data(), text.size());
+  put_blob(f, c.name.data(), c.name.size());
+  put_blob(f, c.code.data(), c.code.size());
+  const int v[5] = {c.vgprs, c.sgprs, c.scratch, c.vspill, c.occupancy};
+  f.append((const char*)v, 20);
+  char tmp[64];
+  snprintf(tmp, sizeof tmp, ".tmp.%d.%llx", (int)getpid(), (unsigned long long)std::hash<std::thread::id>()(std::this_thread::get_id()));
+  const std::string tp = path + tmp;
+  FILE* fo = fopen(tp.c_str(), "wb");
+  if (!fo) return;                                        // the cache is an optimisation: no error
+  const bool ok = fwrite(f.data(), 1, f.size(), fo) == f.size();
+  if (fclose(fo) == 0 && ok) (void)rename(tp.c_str(), path.c_str());
+  else (void)unlink(tp.c_str());
+}
+
+// The code object of one program: the on-disk cache, else hipRTC; then the resource guard.
+int spec_obtain(const std::string& text, SpecCode* out, std::string* err) {
+  const Rtc& R = rtc();
+  if (!R.rocm) {
+    *err = "hipRTC guard: the ROCm installation's libhiprtc could not be loaded into a namespace of its own (" + R.origin +
+           "); another hipRTC in the process (PyTorch bundles an older LLVM) is not used";
+    return RT_ERR_UNSUPPORTED;
+  }
+  std::string dir;
+  {
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    dir = sst().disk_dir;
+  }
+  const std::string path = dir.empty() ? "" : disk_path(dir, R.identity, text);
+  if (!path.empty() && disk_read(path, R.identity, text, out)) return spec_guard(*out, text, err);
+  int rc = spec_compile(text, out, err);
+  if (!rc) rc = spec_guard(*out, text, err);
+  if (!rc && !path.empty()) disk_write(dir, path, R.identity, text, *out);
+  return rc;
+}
+
+void spec_worker() {
+  SpecState& S = sst();
+  for (;;) {
+    std::shared_ptr<SpecJob> j;
+    {
+      std::unique_lock<std::mutex> lk(g_spec_mu);
+      S.qcv.wait(lk, [&] { return S.stop || !S.queue.empty(); });
+      if (S.queue.empty()) return;                        // shut down
+      j = S.queue.front();
+      S.queue.pop_front();
+      if (j->interest.load() == 0) {                      // nobody renders this program any more
+        auto it = S.jobs.find(j->text);
+        if (it != S.jobs.end() && it->second == j) S.jobs.erase(it);
+        job_finish(j.get(), SPEC_CANCELLED);
+        continue;
+      }
+      j->state = SPEC_RUNNING;
+    }
+    std::string err;
+    const int rc = spec_obtain(j->text, &j->code, &err);
+    if (rc) j->error = err;
+    job_finish(j.get(), rc ? SPEC_FAILED : SPEC_DONE);
+  }
+}
+
+// A token for the program `text`: the process's job for it (queued, running or done), or a new job
+// for the pool.  retry: a FAILED job is compiled again.  *was_done: the code object already existed.
+std::shared_ptr<SpecJob> spec_request(const std::string& text, bool retry = false, bool* was_done = nullptr) {
+  std::lock_guard<std::mutex> lk(g_spec_mu);
+  SpecState& S = sst();
+  auto it = S.jobs.find(text);
+  if (it != S.jobs.end()) {
+    const std::shared_ptr<SpecJob> j = it->second;
+    const int st = j->state.load();
+    if (st != SPEC_CANCELLED && !(retry && st == SPEC_FAILED)) {
+      j->last_use = ++S.clock;
+      if (was_done) *was_done = st == SPEC_DONE;
+      return job_token(j);
+    }
+    S.jobs.erase(it);
+  }
+  if (was_done) *was_done = false;
+  auto j = std::make_shared<SpecJob>();
+  j->text = text;
+  j->last_use = ++S.clock;
+  if (S.jobs.size() >= RT_SPEC_CACHE_JOBS) {              // evict the least recently used finished jobs nobody holds
+    std::vector<std::pair<uint64_t, std::string>> idle;
+    for (auto& kv : S.jobs)
+      if (kv.second->interest.load() == 0 && job_finished(kv.second.get())) idle.push_back({kv.second->last_use, kv.first});
+    std::sort(idle.begin(), idle.end());
+    for (size_t i = 0; i < idle.size() && S.jobs.size() >= RT_SPEC_CACHE_JOBS; ++i) S.jobs.erase(idle[i].second);
+  }
+  S.jobs.emplace(text, j);
+  if (S.stop) {
+    j->error = "the specialisation pool is shut down (rt_spec_shutdown)";
+    j->state = SPEC_FAILED;
+    return job_token(j);
+  }
+  S.queue.push_back(j);
+  const size_t want = std::min<size_t>(RT_SPEC_WORKERS_MAX, std::max(1u, std::thread::hardware_concurrency()));
+  if (S.workers.size() < want) S.workers.emplace_back(spec_worker);
+  S.qcv.notify_one();
+  return job_token(j);
+}
+
+}  // namespace
+
+namespace rt {
+
+const char* spec_compiler() { return rtc().origin.c_str(); }
+
+// The flags of an uploaded scene that decide its program (cheap; no text is generated).
+void spec_flags(const FlatScene& f, rt_ctx* c) {
   // The walks unroll over every hierarchy node and leaf, twice (nearest hit, shadows), and the
   // shading over every object: code size and compile time grow with the scene (globes.scene, 6
-  // objects and 11 leaves: ~15 k instructions, ~8 s of hipRTC per kernel).  Larger scenes keep the
+  // objects and 11 leaves: ~15 k instructions, ~3-12 s of hipRTC per kernel).  Larger scenes keep the
   // generic kernels (fractal.scene: 171 objects).
   c->spec_fits = f.objects.size() <= RT_SPEC_MAX_OBJECTS && f.leaves.size() <= RT_SPEC_MAX_LEAVES;
   c->spec_mode = !f.any_transparent ? RT_MODE_REFL : f.ray_chains ? RT_MODE_CHAIN : RT_MODE_TREE;
   c->spec_fc = f.colour_fast != 0;
   c->spec_deferred = c->spec_mode == RT_MODE_REFL;
+}
+
+// The program text of a flattened scene for c's level: a registered family's, or its own.
+static void spec_text(const FlatScene& f, rt_ctx* c) {
+  spec_flags(f, c);
   c->spec_family = 0;
-  {                                    // a registered family holding this scene: its program
+  {
     std::lock_guard<std::mutex> lk(g_spec_mu);
     for (auto it = g_families.rbegin(); it != g_families.rend(); ++it)
       if (family_member(**it, f)) {
@@ -414,49 +746,174 @@ void spec_program(const FlatScene& f, rt_ctx* c) {
   c->spec_src = spec_source(f, nullptr);
 }
 
-int spec_build(rt_ctx* c) {
-  spec_drop(c);
-  if (c->spec_src.empty() || !c->spec_fits) return RT_OK;   // too large to unroll: the generic kernels
-  const std::vector<std::string> srcs = spec_programs(c);
-  std::vector<std::shared_ptr<SpecCode>> codes;
-  int rc = spec_codes(srcs, &codes, &c->spec_compile_ms);
-  if (rc) return rc;
-  RT_HIP(hipSetDevice(c->device));
+void spec_drop(rt_ctx* c) {
+  for (auto& m : c->spec_mods)
+    if (m) (void)hipModuleUnload(m);
+  memset(c->spec_mods, 0, sizeof c->spec_mods);
+  c->spec_mod = nullptr;
+  memset(c->spec_rows, 0, sizeof c->spec_rows);
+  memset(c->spec_def, 0, sizeof c->spec_def);
+  c->spec_jobs.clear();                                   // drops this context's interest
+  c->spec_error.clear();
+}
+
+void spec_prepare(rt_ctx* c, bool retry) {
+  c->spec_jobs.clear();
+  c->spec_error.clear();
+  c->spec_note.clear();
+  if (!c->spec_on || !c->spec_flat || !c->spec_fits) return;
+  spec_text(*c->spec_flat, c);
+  bool all_done = true;
+  for (const std::string& t : spec_programs(c)) {
+    bool done = false;
+    c->spec_jobs.push_back(spec_request(t, retry, &done));
+    all_done = all_done && done;
+  }
+  if (all_done) c->spec_note = " [process cache]";
+  c->spec_t0 = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int spec_poll(rt_ctx* c) {
+  if (c->spec_jobs.empty()) return RT_OK;
+  for (auto& j : c->spec_jobs)
+    if (!job_finished(j.get())) return RT_PENDING;
+  for (auto& j : c->spec_jobs)
+    if (j->state.load() != SPEC_DONE) {
+      c->spec_error = j->state.load() == SPEC_CANCELLED ? "compile cancelled (rt_spec_shutdown)" : j->error;
+      c->spec_jobs.clear();
+      return RT_OK;
+    }
   char name[32];
   const std::vector<SpecKernel> ks = spec_kernels(c);
+  double ms = 0.0;
+  bool disk = false;
+  std::string res;
   for (size_t i = 0; i < ks.size(); ++i) {
     const SpecKernel& k = ks[i];
-    RT_HIP(hipModuleLoadData(&c->spec_mods[i], codes[i]->code.data()));
-    snprintf(name, sizeof name, k.kind ? "rt_spec_def_%d%d" : "rt_spec_rows_%d%d", k.f64, k.cal);
-    RT_HIP(hipModuleGetFunction(k.kind ? &c->spec_def[k.f64][k.cal] : &c->spec_rows[k.f64][k.cal], c->spec_mods[i], name));
+    const SpecCode& code = c->spec_jobs[i]->code;
+    hipError_t e = hipModuleLoadData(&c->spec_mods[i], code.code.data());
+    if (e == hipSuccess) {
+      snprintf(name, sizeof name, k.kind ? "rt_spec_def_%d%d" : "rt_spec_rows_%d%d", k.f64, k.cal);
+      e = hipModuleGetFunction(k.kind ? &c->spec_def[k.f64][k.cal] : &c->spec_rows[k.f64][k.cal], c->spec_mods[i], name);
+    }
+    if (e != hipSuccess) {
+      c->spec_jobs.clear();
+      spec_drop(c);
+      c->spec_error = std::string("loading the specialised code object failed: ") + hipGetErrorString(e);
+      return RT_OK;
+    }
+    ms = std::max(ms, code.compile_ms);
+    disk = disk || code.from_disk;
+    if (i == 0) {
+      char b[160];
+      snprintf(b, sizeof b, "%d VGPRs (%d spilled), %d B/lane scratch", code.vgprs, code.vspill, code.scratch);
+      res = b;
+    }
   }
   c->spec_mod = c->spec_mods[0];
   c->spec_hash = fnv1a(c->spec_src);
+  c->spec_compile_ms = ms;
+  c->spec_res = res;
+  if (disk && c->spec_note.empty()) c->spec_note = " [disk cache]";
+  c->spec_ready_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count() -
+                     c->spec_t0;
+  c->spec_jobs.clear();
+  // Orders built while the generic kernels ran may have chosen the deferred kernel for a tail-bound
+  // launch (split entries); with the specialised megakernel loaded that choice no longer pays
+  // (k_rows.hip): those geometries calibrate again.
+  for (auto& s : c->order)
+    if (s.valid && s.deferred) drop_order(s);
   return RT_OK;
+}
+
+int spec_wait(rt_ctx* c, double timeout_ms) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (auto& j : c->spec_jobs) {
+    double left = -1.0;
+    if (timeout_ms >= 0)
+      left = std::max(0.0, timeout_ms - std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    if (!job_wait(j.get(), left)) return RT_PENDING;
+  }
+  return spec_poll(c);
 }
 
 }  // namespace rt
 
-// rt_scene_precompile (include/rt_abi.h): the specialised programs of a scene into the process cache,
-// no device needed -- a host may compile on a worker thread while it renders with the generic kernels
-extern "C" int rt_scene_precompile(const rt_scene* s, double* compile_ms) {
+// Waits for every job (no limit); the longest fresh compile in *ms (0: all came from a cache); the
+// first failure's status and message.
+static int wait_all(const std::vector<std::shared_ptr<SpecJob>>& jobs, const std::vector<bool>& was_done, double* ms) {
+  *ms = 0.0;
+  for (size_t i = 0; i < jobs.size(); ++i) {
+    job_wait(jobs[i].get(), -1.0);
+    if (jobs[i]->state.load() != SPEC_DONE)
+      return fail(RT_ERR_UNSUPPORTED, "%s", jobs[i]->state.load() == SPEC_CANCELLED ? "compile cancelled (rt_spec_shutdown)"
+                                                                                   : jobs[i]->error.c_str());
+    if (!was_done[i]) *ms = std::max(*ms, jobs[i]->code.compile_ms);
+  }
+  return RT_OK;
+}
+
+// The programs of scene s at level `level` (tmp context), requested from the pool.
+static int scene_jobs(const rt_scene* s, int level, rt_ctx* tmp, std::vector<std::shared_ptr<SpecJob>>* jobs,
+                      std::vector<bool>* was_done) {
   if (!s) return fail(RT_ERR_INVALID, "null scene");
   rt::FlatScene f;
   int rc = rt::flatten(*s, &f);
   if (rc) return rc;
-  rt_ctx tmp;
-  tmp.spec_on = 1;
-  rt::spec_program(f, &tmp);
-  if (!tmp.spec_fits) {
-    if (compile_ms) *compile_ms = 0.0;
+  tmp->spec_on = level;
+  rt::spec_text(f, tmp);
+  if (!tmp->spec_fits)
     return fail(RT_ERR_UNSUPPORTED, "scene of %zu objects / %zu leaves is not specialised (limits %d / %d)",
                 f.objects.size(), f.leaves.size(), RT_SPEC_MAX_OBJECTS, RT_SPEC_MAX_LEAVES);
+  for (const std::string& t : rt::spec_programs(tmp)) {
+    bool done = false;
+    jobs->push_back(spec_request(t, false, &done));
+    was_done->push_back(done);
   }
-  std::vector<std::shared_ptr<SpecCode>> codes;
+  return RT_OK;
+}
+
+// rt_scene_precompile (include/rt_abi.h): the specialised programs of a scene into the process cache,
+// no device needed -- a host may compile on a worker thread while it renders with the generic kernels
+extern "C" int rt_scene_precompile(const rt_scene* s, double* compile_ms) {
+  rt_ctx tmp;
+  std::vector<std::shared_ptr<SpecJob>> jobs;
+  std::vector<bool> done;
   double ms = 0.0;
-  rc = rt::spec_codes(rt::spec_programs(&tmp), &codes, &ms);
+  int rc = scene_jobs(s, 1, &tmp, &jobs, &done);
+  if (!rc) rc = wait_all(jobs, done, &ms);
   if (compile_ms) *compile_ms = ms;
   return rc;
+}
+
+// rt_scene_spec_report (include/rt_abi.h): compile (or find) the scene's level-1 programs and describe
+// them: the compiler, and per kernel its resource use and how it was obtained
+extern "C" int rt_scene_spec_report(const rt_scene* s, char* buf, size_t cap, size_t* len) {
+  if (!len || (cap > 0 && !buf)) return fail(RT_ERR_INVALID, "null argument");
+  rt_ctx tmp;
+  std::vector<std::shared_ptr<SpecJob>> jobs;
+  std::vector<bool> done;
+  double ms = 0.0;
+  int rc = scene_jobs(s, 1, &tmp, &jobs, &done);
+  if (!rc) rc = wait_all(jobs, done, &ms);
+  if (rc) return rc;
+  // source: how the code object was made -- by hipRTC in this process, or read from the disk cache
+  std::string text = "compiler: " + rtc().identity + (rtc().rocm ? " (the ROCm installation's hipRTC)" : "") + "\n";
+  for (size_t i = 0; i < jobs.size(); ++i) {
+    const SpecCode& c = jobs[i]->code;
+    char line[512];
+    snprintf(line, sizeof line, "%s: vgprs %d spilled %d sgprs %d scratch %d occupancy %d code %zu compile_ms %.0f source %s\n",
+             c.name.c_str(), c.vgprs, c.vspill, c.sgprs, c.scratch, c.occupancy, c.code.size(), c.compile_ms,
+             c.from_disk ? "disk" : "hiprtc");
+    text += line;
+  }
+  *len = text.size();
+  if (cap > 0) {
+    const size_t n = text.size() < cap - 1 ? text.size() : cap - 1;
+    memcpy(buf, text.data(), n);
+    buf[n] = 0;
+  }
+  return RT_OK;
 }
 
 // rt_scene_spec_program (include/rt_abi.h): the prelude and every kernel rt_scene_precompile compiles
@@ -467,7 +924,7 @@ extern "C" int rt_scene_spec_program(const rt_scene* s, char* buf, size_t cap, s
   if (rc) return rc;
   rt_ctx tmp;
   tmp.spec_on = 2;
-  rt::spec_program(f, &tmp);
+  rt::spec_text(f, &tmp);
   std::string text = tmp.spec_src;
   for (const rt::SpecKernel& k : rt::spec_kernels(&tmp)) text += rt::spec_kernel(k.kind, tmp.spec_mode, tmp.spec_fc, k.f64, k.cal);
   *len = text.size();
@@ -482,7 +939,7 @@ extern "C" int rt_scene_spec_program(const rt_scene* s, char* buf, size_t cap, s
 // rt_spec_family_register (include/rt_abi.h): specialised programs for n scenes (the frames of an
 // animation), one per class of scenes of the same structure and object hierarchy (the frames of
 // spinning_globes.scene fall in two: the hierarchy's grouping follows the globes' positions);
-// contexts whose scene belongs to a class load its program (spec_program).
+// contexts whose scene belongs to a class load its program (spec_text).
 static bool same_hierarchy(const std::vector<RtTrav>& a, const std::vector<RtTrav>& b) {
   if (a.size() != b.size()) return false;
   for (size_t i = 0; i < a.size(); ++i)
@@ -490,6 +947,7 @@ static bool same_hierarchy(const std::vector<RtTrav>& a, const std::vector<RtTra
   return true;
 }
 extern "C" int rt_spec_family_register(const rt_scene* const* scenes, int32_t n, double* compile_ms) {
+  if (compile_ms) *compile_ms = 0.0;
   if (!scenes || n < 1) return fail(RT_ERR_INVALID, "no scenes");
   std::vector<std::shared_ptr<SpecFamily>> fams;
   rt::FlatScene f;
@@ -505,6 +963,9 @@ extern "C" int rt_spec_family_register(const rt_scene* const* scenes, int32_t n,
         break;
       }
     if (!F) {
+      if (fams.size() >= RT_SPEC_MAX_FAMILIES)             // every family is a compile: bounded per call
+        return fail(RT_ERR_UNSUPPORTED, "the scenes form more than %d families (structure or object hierarchy differ)",
+                    RT_SPEC_MAX_FAMILIES);
       fams.push_back(std::make_shared<SpecFamily>());
       F = fams.back().get();
       F->base = f;
@@ -516,31 +977,102 @@ extern "C" int rt_spec_family_register(const rt_scene* const* scenes, int32_t n,
     vary_words(F->base.leaves, f.leaves, &F->v_leaf);
     vary_words(F->base.lights, f.lights, &F->v_light);
   }
-  std::vector<std::string> srcs;
-  for (auto& F : fams) {
+  // A family of ONE scene gets no family program: the scene's own program (every word a constant, the
+  // tables in the constant address space) is the better code -- globes.scene as a family of one
+  // spilled to 1 392 B/lane of scratch (its own program: 560) -- so its own program is compiled now.
+  std::vector<std::shared_ptr<SpecJob>> all;
+  std::vector<bool> done;
+  std::vector<size_t> first(fams.size());
+  for (size_t fi = 0; fi < fams.size(); ++fi) {
+    auto& F = fams[fi];
     rt_ctx tmp;
     tmp.spec_on = 1;
-    rt::spec_program(F->base, &tmp);             // mode / clamp form / size limits of the class
+    rt::spec_flags(F->base, &tmp);                 // mode / clamp form / size limits of the class
     if (!tmp.spec_fits)
       return fail(RT_ERR_UNSUPPORTED, "scenes of %zu objects / %zu leaves are not specialised (limits %d / %d)",
                   F->base.objects.size(), F->base.leaves.size(), RT_SPEC_MAX_OBJECTS, RT_SPEC_MAX_LEAVES);
-    F->src = rt::spec_source(F->base, F.get());
+    F->src = rt::spec_source(F->base, F->members > 1 ? F.get() : nullptr);
     tmp.spec_src = F->src;
-    for (std::string& s : rt::spec_programs(&tmp)) srcs.push_back(std::move(s));
+    first[fi] = all.size();
+    for (const std::string& t : rt::spec_programs(&tmp)) {
+      bool d = false;
+      F->jobs.push_back(spec_request(t, false, &d));
+      all.push_back(F->jobs.back());
+      done.push_back(d);
+    }
   }
-  std::vector<std::shared_ptr<SpecCode>> codes;   // every class's programs, compiled in parallel
+  // every class's programs, compiled by the pool in parallel; the families whose programs compiled and
+  // passed the guard are registered, the others not (their scenes then compile their own programs)
   double ms = 0.0;
-  int rc = rt::spec_codes(srcs, &codes, &ms);
+  std::string first_err;
+  std::vector<char> good(fams.size(), 0);
+  for (size_t fi = 0; fi < fams.size(); ++fi) {
+    bool ok = true;
+    for (size_t i = first[fi]; i < first[fi] + fams[fi]->jobs.size(); ++i) {
+      job_wait(all[i].get(), -1.0);
+      if (all[i]->state.load() != SPEC_DONE) {
+        ok = false;
+        if (first_err.empty())
+          first_err = "family of " + std::to_string(fams[fi]->members) + " scenes: " +
+                      (all[i]->state.load() == SPEC_CANCELLED ? std::string("compile cancelled (rt_spec_shutdown)") : all[i]->error);
+      } else if (!done[i]) {
+        ms = std::max(ms, all[i]->code.compile_ms);
+      }
+    }
+    good[fi] = ok;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    for (size_t fi = 0; fi < fams.size(); ++fi)
+      if (good[fi]) (fams[fi]->members > 1 ? g_families : g_singles).push_back(fams[fi]);   // singles: their own program resident
+  }
   if (compile_ms) *compile_ms = ms;
-  if (rc) return rc;
-  std::lock_guard<std::mutex> lk(g_spec_mu);
-  for (auto& F : fams) g_families.push_back(F);
+  if (!first_err.empty()) return fail(RT_ERR_UNSUPPORTED, "%s", first_err.c_str());
   return RT_OK;
 }
 
 // rt_spec_family_clear (include/rt_abi.h): forget every registered family (loaded modules stay)
 extern "C" int rt_spec_family_clear(void) {
+  std::vector<std::shared_ptr<SpecFamily>> old, old1;
+  {
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    old.swap(g_families);
+    old1.swap(g_singles);
+  }
+  return RT_OK;                                    // `old` drops the families' interest in their programs
+}
+
+// rt_spec_cache_dir (include/rt_abi.h): the on-disk code-object cache ("" or NULL: none)
+extern "C" int rt_spec_cache_dir(const char* dir) {
   std::lock_guard<std::mutex> lk(g_spec_mu);
-  g_families.clear();
+  sst().disk_dir = dir ? dir : "";
+  while (sst().disk_dir.size() > 1 && sst().disk_dir.back() == '/') sst().disk_dir.pop_back();
   return RT_OK;
+}
+
+// rt_spec_compiler_info (include/rt_abi.h): which hipRTC the programs compile with
+extern "C" int rt_spec_compiler_info(char* buf, size_t cap, int32_t* rocm) {
+  const Rtc& R = rtc();
+  if (rocm) *rocm = R.rocm ? 1 : 0;
+  if (buf && cap > 0) snprintf(buf, cap, "%s", R.identity.c_str());
+  return RT_OK;
+}
+
+// rt_spec_shutdown (include/rt_abi.h): cancel queued compiles, wait for running ones, stop the pool
+extern "C" void rt_spec_shutdown(void) {
+  std::vector<std::thread> th;
+  {
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    SpecState& S = sst();
+    S.stop = true;
+    for (auto& j : S.queue) {
+      auto it = S.jobs.find(j->text);
+      if (it != S.jobs.end() && it->second == j) S.jobs.erase(it);
+      job_finish(j.get(), SPEC_CANCELLED);
+    }
+    S.queue.clear();
+    th.swap(S.workers);
+    S.qcv.notify_all();
+  }
+  for (auto& t : th) t.join();
 }

@@ -182,6 +182,15 @@ class Scene:
         check(lib().rt_scene_precompile(self.h, ctypes.byref(ms)))
         return ms.value
 
+    def spec_report(self) -> str:
+        """rt_scene_spec_report: compile (or find) the scene's specialised programs and describe them --
+        the compiler, and per kernel its VGPRs, spills, scratch, occupancy and where it came from."""
+        n = ctypes.c_size_t()
+        check(lib().rt_scene_spec_report(self.h, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        check(lib().rt_scene_spec_report(self.h, buf, n.value + 1, ctypes.byref(n)))
+        return buf.value.decode()
+
     @staticmethod
     def register_family(scenes) -> float:
         """rt_spec_family_register: one specialised program for scenes of the same structure (the
@@ -223,13 +232,23 @@ class Scene:
 class Renderer:
     """Owner of an ``rt_ctx*``: one device, its stream, the uploaded scene."""
 
-    def __init__(self, device: int = 0):
+    # RT_OPT_SPECIALIZE for new renderers: None keeps the library's default (1: the scene's kernels
+    # compiled in the background after each upload, taken once ready).  tests/conftest.py sets 0 so
+    # that tests which pin a kernel choice see a deterministic one; the specialised paths have tests of
+    # their own (tests/test_gpu_spec*.py, test_gpu_spec_async.py).
+    LIBRARY_DEFAULT = -1            # specialize=LIBRARY_DEFAULT: leave the option as the library sets it
+    default_specialize: Optional[int] = None
+
+    def __init__(self, device: int = 0, specialize: Optional[int] = None):
         h = ctypes.c_void_p()
         check(lib().rt_ctx_create(int(device), ctypes.byref(h)))
         self.h = h
         Renderer._register(self)
         self.device = device
         self.width = self.height = 0
+        level = specialize if specialize is not None else Renderer.default_specialize
+        if level is not None and level != Renderer.LIBRARY_DEFAULT:
+            self.set_specialize(level, wait=False)
 
     def upload(self, scene: Scene) -> None:
         check(lib().rt_ctx_upload(self.h, scene.h))
@@ -356,21 +375,30 @@ class Renderer:
         object, 2 every level (same pixels)."""
         check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_WAVEFRONT_PAIRS, int(mode)))
 
-    def set_specialize(self, level: int = 1) -> None:
-        """rt_ctx_set_option(RT_OPT_SPECIALIZE): 0 the precompiled kernels; 1 compile the uploaded scene's
-        RGBA8 / RGB8 row kernels with the scene as constants (hipRTC, seconds per new scene; same pixels);
-        2 its f64 and calibration kernels too."""
+    def set_specialize(self, level: int = 1, wait: bool = True) -> None:
+        """rt_ctx_set_option(RT_OPT_SPECIALIZE): 0 the precompiled kernels; 1 (the library default) the
+        uploaded scene's RGBA8 / RGB8 row kernels compiled with the scene as constants (hipRTC in the
+        library's background pool; same pixels); 2 its f64 and calibration kernels too.  ``wait``: block
+        until the program is loaded (spec_wait), raising if it failed."""
         check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_SPECIALIZE, int(level)))
+        if wait and level:
+            self.spec_wait()
 
-    def set_tail_tiles(self, tiles: int = 64) -> None:
-        """rt_ctx_set_option(RT_OPT_TAIL_TILES): tiles a tail-bound launch of a reflection-only scene hands to
-        the tail kernel (several lanes per pixel, its own hardware queue); 0 none (same pixels)."""
-        check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_TAIL_TILES, int(tiles)))
+    def set_tiles_per_wave(self, n: int = 0) -> None:
+        """rt_ctx_set_option(RT_OPT_TILES_PER_WAVE): 8x8 tiles per wave of the specialised megakernel
+        (0 = the calibration's choice; same pixels)."""
+        check(lib().rt_ctx_set_option(self.h, _lib.RT_OPT_TILES_PER_WAVE, int(n)))
+
+    def spec_wait(self, timeout_ms: int = -1) -> bool:
+        """rt_ctx_spec_wait: block until the scene-specialised program is loaded (True), or until
+        ``timeout_ms`` passed (False); raises RtError when the compile failed or the guard refused it."""
+        rc = check(lib().rt_ctx_spec_wait(self.h, int(timeout_ms)))
+        return rc != _lib.RT_PENDING
 
     def kernel_info(self) -> str:
         """rt_ctx_kernel_info: generic or scene-specialised kernels, and what the last row launch ran."""
-        buf = ctypes.create_string_buffer(512)
-        check(lib().rt_ctx_kernel_info(self.h, buf, 512))
+        buf = ctypes.create_string_buffer(4096)
+        check(lib().rt_ctx_kernel_info(self.h, buf, 4096))
         return buf.value.decode()
 
     def kernel_variant(self) -> str:
@@ -394,19 +422,25 @@ class Renderer:
     # (atexit runs last-registered first) and so while the HIP runtime is still up: a context freed
     # during module teardown unloaded its specialised modules / freed its buffers after torch had
     # shut its side of the runtime down (round 4: SIGSEGV / std::bad_variant_access at exit).
+    # The hook is moved to the END of the atexit list whenever a renderer is made (atexit runs the
+    # last-registered first), so it still runs before hooks that torch registers once its CUDA side
+    # starts; it also stops the library's compile pool (rt_spec_shutdown) so that no hipRTC compile
+    # runs while the process tears the runtime down.
     @classmethod
     def _register(cls, r: "Renderer") -> None:
+        import atexit
         if "_live" not in cls.__dict__:
-            import atexit
             import weakref
             cls._live = weakref.WeakSet()
-            atexit.register(cls.free_all)
+        atexit.unregister(cls.free_all)
+        atexit.register(cls.free_all)
         cls._live.add(r)
 
     @classmethod
     def free_all(cls) -> None:
         for r in list(cls.__dict__.get("_live", ())):
             r.free()
+        lib().rt_spec_shutdown()
 
     def __del__(self):
         if _sys.is_finalizing():
@@ -628,6 +662,20 @@ def device_count() -> int:
     n = ctypes.c_int()
     check(lib().rt_device_count(ctypes.byref(n)))
     return n.value
+
+
+def spec_compiler_info() -> Tuple[str, bool]:
+    """rt_spec_compiler_info: (identity of the hipRTC the specialised programs compile with, True when
+    it is the ROCm installation's own -- the only one the library lets compile them)."""
+    buf = ctypes.create_string_buffer(1024)
+    rocm = ctypes.c_int32()
+    check(lib().rt_spec_compiler_info(buf, 1024, ctypes.byref(rocm)))
+    return buf.value.decode(), bool(rocm.value)
+
+
+def spec_cache_dir(path: Optional[str]) -> None:
+    """rt_spec_cache_dir: the on-disk code-object cache of the specialised programs (None: none)."""
+    check(lib().rt_spec_cache_dir(path.encode() if path else None))
 
 
 class HwStream:
