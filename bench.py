@@ -444,9 +444,21 @@ def main():
             free_ev[b] = torch.cuda.Event()
             free_ev[b].record(astream)
 
+    # N = 1: each (buffer, stream) pair's launch pre-bound (Renderer.rows_launcher): one ctypes call per
+    # frame, as a native host's FFI call, not the Python wrapper's per-call argument handling
+    launchers = [rend.rows_launcher(0, H, frames[b], max_depth=depth, stream=rstreams[b % K]) for b in range(nbuf)] \
+        if not multi else []
+
     def step(i, ev0=None, ev1=None):
         b = i % nbuf
         s = rstreams[i % K]
+        if not multi and free_ev[b] is None:
+            if ev0 is not None:
+                ev0.record(s)
+            launchers[b]()
+            if ev1 is not None:
+                ev1.record(s)
+            return
         with torch.cuda.stream(s):
             if free_ev[b] is not None:
                 s.wait_event(free_ev[b])                  # slot / gather / frame buffers reusable
@@ -704,9 +716,10 @@ def inflight_phase(T, rend, stream, dev, frame, whole, H, W, depth, local, K, st
         if i % (8 * K) == 0:
             torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
+    launch = [rend.rows_launcher(0, H, bufs[k], max_depth=depth, stream=ss[k]) for k in range(K)]
     t0 = time.perf_counter()
     for i in range(steps):
-        rend.render_rows(0, H, max_depth=depth, out=bufs[i % K], stream=ss[i % K])
+        launch[i % K]()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     bad = [b for b in range(K) if not torch.equal(bufs[b], whole)]
@@ -980,12 +993,14 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
     streams = [torch.cuda.current_stream(dev)] if K == 1 else [h.torch for h in hw]
     torch.cuda.synchronize(dev)
 
+    launch = [r.rows_launcher(0, H, outs[j], max_depth=depth, stream=streams[j % K]) for j, r in enumerate(rends)]
+
     def step(evs=None):
-        for j, r in enumerate(rends):
+        for j in range(len(rends)):
             stream = streams[j % K]
             if evs is not None:
                 evs[j][0].record(stream)
-            r.render_rows(0, H, max_depth=depth, out=outs[j], stream=stream)
+            launch[j]()
             if evs is not None:
                 evs[j][1].record(stream)
 
@@ -998,14 +1013,17 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
+    # one stream: an event pair per frame gives the frames' kernel times; several streams: no events in
+    # the timed region (each timed event costs its stream ~5 us, profiles/r02dc_launch_events.txt, and
+    # the roofline is taken over wall time then) -- the per-frame times come from one untimed step after
     evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in mine]
-           for _ in range(a.steps)]
+           for _ in range(a.steps if K == 1 else 1)]
     if multi:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step(evs[i])
+        step(evs[i] if K == 1 else None)
     torch.cuda.synchronize(dev)
     if multi:
         dist.barrier()
@@ -1014,7 +1032,10 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
         e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    per_frame = [sum(evs[i][j][0].elapsed_time(evs[i][j][1]) for i in range(a.steps)) / a.steps
+    if K > 1:
+        step(evs[0])                                      # untimed: the frames' kernel times
+        torch.cuda.synchronize(dev)
+    per_frame = [sum(evs[i][j][0].elapsed_time(evs[i][j][1]) for i in range(len(evs))) / len(evs)
                  for j in range(len(mine))]
     # outside the timed region: every owned frame buffer == a single-launch render of its frame
     bad = []
@@ -1073,7 +1094,8 @@ def anim_main(a, json_out, rank, world, local, dev, multi, rehearse=False):
                                    load_traffic(a.config, 1, "contiguous"), {
             "kernel": rends[0].kernel_info() + " (ray-chain scene; RT_OPT_KERNEL " + a.kernel + ")",
             "streams": K,
-            "achieved_basis": "kernel event time" if K == 1 else "step wall time (frames overlap on the streams)",
+            "achieved_basis": "kernel event time" if K == 1 else "step wall time (frames overlap on the streams; "
+                              "kernel_ms_*: one untimed step with events, overlapped)",
             "kernel_ms_mean": round(sum(per_frame) / len(per_frame), 4),
             "kernel_ms_min": round(min(per_frame), 4),
             "kernel_ms_max": round(max(per_frame), 4),

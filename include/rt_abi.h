@@ -291,13 +291,10 @@ int rt_ctx_synchronize(rt_ctx* ctx);
  * value again after a failure retries the compile.  Launches whose kernel has no specialised form
  * (wavefront, refraction deferred, RT_OPT_FAST_CLAMP 0 on a min/max-clamp scene) keep the generic
  * kernels.
- * RT_OPT_TILES_PER_WAVE: the specialised megakernel takes its 8x8 tiles grid-stride, this many per
- * wave (1..16); 0 (default) lets the calibration choose from the launch's tile costs (cheap launches,
- * e.g. primary rays only, take several: a wave's dispatch then serves more pixels).  Same pixels.
  * Option 7 is retired (round 4's tail kernel, measured slower than the launch it shortened). */
 typedef enum rt_option {
   RT_OPT_KERNEL = 0, RT_OPT_TIMING = 1, RT_OPT_TILE_ORDER = 2, RT_OPT_FAST_CLAMP = 3, RT_OPT_WAVEFRONT_CAP = 4,
-  RT_OPT_WAVEFRONT_PAIRS = 5, RT_OPT_SPECIALIZE = 6, RT_OPT_TILES_PER_WAVE = 8
+  RT_OPT_WAVEFRONT_PAIRS = 5, RT_OPT_SPECIALIZE = 6
 } rt_option;
 typedef enum rt_kernel_choice {
   RT_KERNEL_AUTO = 0, RT_KERNEL_MEGA = 1, RT_KERNEL_DEFERRED = 2, RT_KERNEL_WAVEFRONT = 3

@@ -27,7 +27,6 @@ RT_OPT_FAST_CLAMP = 3
 RT_OPT_WAVEFRONT_CAP = 4
 RT_OPT_WAVEFRONT_PAIRS = 5
 RT_OPT_SPECIALIZE = 6
-RT_OPT_TILES_PER_WAVE = 8
 RT_KERNEL_AUTO, RT_KERNEL_MEGA, RT_KERNEL_DEFERRED, RT_KERNEL_WAVEFRONT = 0, 1, 2, 3
 
 

@@ -9,6 +9,7 @@
 
 #include "rt_device.h"
 #include "rt_ctx.h"
+#include <hip/hip_ext.h>
 
 namespace {
 
@@ -159,24 +160,31 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   else if (calibrate) deferred = false;                       // calibrate on the megakernel
   else deferred = n_tiles < RT_ORDER_MIN_TILES || (!c->tile_order && n_tiles < RT_DEFERRED_MAX_TILES);
   if (c->timing) RT_HIP(hipEventRecord(c->ev0, st));
+  // the row kernels carry the context's completion event for this stream as their stop event
+  hipEvent_t mev = nullptr;
+#ifndef RT_DIAG_NO_MARKS
+  RT_TRY(mark_event(c, st, &mev));
+#endif
 #define RT_LAUNCH_ROWS(R, F)                                                                                  \
-  if (calibrate && fc) hipLaunchKernelGGL((render_rows_kernel<R, F, true, true>), grid, block, 0, st, c->dev, a0, a1, \
-                                          a2, a3, max_depth, target, tstride, order, cost, rgbi);                       \
-  else if (calibrate) hipLaunchKernelGGL((render_rows_kernel<R, F, true, false>), grid, block, 0, st, c->dev, a0, a1, \
-                                         a2, a3, max_depth, target, tstride, order, cost, rgbi);                        \
-  else if (fc) hipLaunchKernelGGL((render_rows_kernel<R, F, false, true>), grid, block, 0, st, c->dev, a0, a1, a2, a3, \
-                                  max_depth, target, tstride, order, cost, rgbi);                                       \
-  else hipLaunchKernelGGL((render_rows_kernel<R, F, false, false>), grid, block, 0, st, c->dev, a0, a1, a2, a3,   \
-                          max_depth, target, tstride, order, cost, rgbi);
+  if (calibrate && fc) hipExtLaunchKernelGGL((render_rows_kernel<R, F, true, true>), grid, block, 0, st, nullptr, mev, 0, \
+                                             c->dev, a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);     \
+  else if (calibrate) hipExtLaunchKernelGGL((render_rows_kernel<R, F, true, false>), grid, block, 0, st, nullptr, mev, 0, \
+                                            c->dev, a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);      \
+  else if (fc) hipExtLaunchKernelGGL((render_rows_kernel<R, F, false, true>), grid, block, 0, st, nullptr, mev, 0, c->dev, \
+                                     a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);                     \
+  else hipExtLaunchKernelGGL((render_rows_kernel<R, F, false, false>), grid, block, 0, st, nullptr, mev, 0, c->dev, a0, a1, \
+                             a2, a3, max_depth, target, tstride, order, cost, rgbi);
 #define RT_LAUNCH_DEFERRED(F, R)                                                                                \
-  if (calibrate && fc) hipLaunchKernelGGL((render_rows_deferred_kernel<F, true, true, R>), grid, dim3(64), 0, st,    \
-                                          c->dev, a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);     \
-  else if (calibrate) hipLaunchKernelGGL((render_rows_deferred_kernel<F, true, false, R>), grid, dim3(64), 0, st,    \
-                                         c->dev, a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);      \
-  else if (fc) hipLaunchKernelGGL((render_rows_deferred_kernel<F, false, true, R>), grid, dim3(64), 0, st, c->dev,   \
-                                  a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);                     \
-  else hipLaunchKernelGGL((render_rows_deferred_kernel<F, false, false, R>), grid, dim3(64), 0, st, c->dev, a0, a1,  \
-                          a2, a3, max_depth, target, tstride, order, cost, rgbi);
+  if (calibrate && fc) hipExtLaunchKernelGGL((render_rows_deferred_kernel<F, true, true, R>), grid, dim3(64), 0, st,     \
+                                             nullptr, mev, 0, c->dev, a0, a1, a2, a3, max_depth, target, tstride, order,  \
+                                             cost, rgbi);                                                                 \
+  else if (calibrate) hipExtLaunchKernelGGL((render_rows_deferred_kernel<F, true, false, R>), grid, dim3(64), 0, st,     \
+                                            nullptr, mev, 0, c->dev, a0, a1, a2, a3, max_depth, target, tstride, order,   \
+                                            cost, rgbi);                                                                  \
+  else if (fc) hipExtLaunchKernelGGL((render_rows_deferred_kernel<F, false, true, R>), grid, dim3(64), 0, st, nullptr,   \
+                                     mev, 0, c->dev, a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);      \
+  else hipExtLaunchKernelGGL((render_rows_deferred_kernel<F, false, false, R>), grid, dim3(64), 0, st, nullptr, mev, 0,   \
+                             c->dev, a0, a1, a2, a3, max_depth, target, tstride, order, cost, rgbi);
   const bool fc = c->dev.colour_fast != 0 && c->fast_clamp;
   // Ray-tree scenes (a transparent AND reflective object) under RT_KERNEL_AUTO: the first ordered
   // launch of a geometry is timed against one wavefront launch of the same rows, and the faster
@@ -205,16 +213,10 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
     sfn = deferred ? c->spec_def[f64 ? 1 : 0][calibrate ? 1 : 0] : c->spec_rows[f64 ? 1 : 0][calibrate ? 1 : 0];
   c->last_kernel = deferred ? (sfn ? "deferred (specialised)" : "deferred") : (sfn ? "megakernel (specialised)" : "megakernel");
   if (sfn) {
-    // the specialised megakernel takes its entries grid-stride: `tpw` entries per wave for launches
-    // whose tiles are cheap (RT_OPT_TILES_PER_WAVE; the calibration's choice by default)
-    unsigned n_entries = grid.x, wgs = grid.x;
-    if (!deferred) {
-      const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : slot && slot->valid && !calibrate ? slot->tpw : 1;
-      wgs = (n_entries + (unsigned)tpw - 1) / (unsigned)tpw;
-    }
     void* kargs[] = {&c->dev, (void*)&a0, (void*)&a1, (void*)&a2, (void*)&a3, &max_depth, &target, &tstride,
-                     (void*)&order, &cost, (void*)&rgbi, &n_entries};
-    RT_HIP(hipModuleLaunchKernel(sfn, wgs, 1, 1, 64, 1, 1, 0, st, kargs, nullptr));
+                     (void*)&order, &cost, (void*)&rgbi};
+    // hipExtModuleLaunchKernel takes the global work size in work-items (grid x 64)
+    RT_HIP(hipExtModuleLaunchKernel(sfn, grid.x * 64u, 1, 1, 64, 1, 1, 0, st, kargs, nullptr, nullptr, mev, 0));
   }
   else if (deferred && chain && f64) { RT_LAUNCH_DEFERRED(true, true) }
   else if (deferred && chain) { RT_LAUNCH_DEFERRED(false, true) }
@@ -231,7 +233,6 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   RT_HIP(hipGetLastError());
   if (c->timing) RT_HIP(hipEventRecord(c->ev1, st));
   c->timed = c->timing;
-  RT_TRY(mark_launch(c, st));
   if (tune) {                         // synchronous, once per ray-tree geometry (see above)
     float mega_ms = 0.0f, wf_ms = 0.0f;
     RT_HIP(hipEventRecord(c->tev1, st));

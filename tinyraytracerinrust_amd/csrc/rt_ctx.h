@@ -25,7 +25,6 @@ struct rt_ctx {
   bool timing = true;                   // rt_ctx_set_option(RT_OPT_TIMING): launch events recorded
   bool tile_order = true;               // rt_ctx_set_option(RT_OPT_TILE_ORDER): cost-ordered dispatch
   bool fast_clamp = true;               // rt_ctx_set_option(RT_OPT_FAST_CLAMP): min/max clamps where exact
-  int tiles_per_wave = 0;               // rt_ctx_set_option(RT_OPT_TILES_PER_WAVE): 0 auto (calibration), 1..16
   int wf_cap_pct = 200;                 // rt_ctx_set_option(RT_OPT_WAVEFRONT_CAP): rays per level, % of pixel slots
   double wf_klo[3] = {-100, -100, -100}, wf_khi[3] = {100, 100, 100};   // coherence-key extent (bounded objects)
   int n_cu = 256;                       // compute units of the device (wave slots = n_cu x 4 SIMDs x waves/SIMD)
@@ -60,7 +59,6 @@ struct rt_ctx {
     bool deferred = false;            // ordered launches take the deferred-shadow kernel
     int wf_tune = 0;                  // ray-tree scenes, RT_KERNEL_AUTO: 0 not yet timed, 1 megakernel, 2 wavefront
     bool valid = false;               // set once the sorted order is on the device
-    int tpw = 1;                      // entries per wave of the specialised megakernel (cheap tiles: several)
   };
   static constexpr int RT_ORDER_SLOTS = 8;
   OrderSlot order[RT_ORDER_SLOTS];
@@ -130,7 +128,8 @@ bool diag_env(const char* name);
 int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int a3, int max_depth, uint8_t* target,
                      size_t tstride, bool f64, int rgbi, size_t n_tiles);
 // Completion marks (rt_ctx.hip): record one after every launch of the context on stream st; wait for all
-int mark_launch(rt_ctx* c, hipStream_t st);
+int mark_event(rt_ctx* c, hipStream_t st, hipEvent_t* ev);   // the event a launch on st binds as its stop event
+int mark_launch(rt_ctx* c, hipStream_t st);                  // record it after work enqueued on st (other launches)
 int wait_launches(rt_ctx* c);
 // spec.hip: the specialised programs of the uploaded scene -- flags (at upload, cheap), the request to the
 // compile pool (asynchronous), the load once compiled (at the next launch, or spec_wait), release

@@ -39,14 +39,19 @@ int ensure_scratch(rt_ctx* c, size_t bytes) {
   return RT_OK;
 }
 
-int mark_launch(rt_ctx* c, hipStream_t st) {
+// The completion event of stream st for c (created on first use; with more than 16 streams the
+// least recently added one's launches are waited for and its event reused).  Row launches BIND it to
+// the kernel dispatch itself (hipExtLaunchKernel's stop event: no marker packet of its own); a
+// separate hipEventRecord after every launch cost the stream 2.5-3.6 us per launch
+// (profiles/r07d_marks_ab.txt: the 1080p sphere 0.0189 -> 0.0218 ms per frame).
+int mark_event(rt_ctx* c, hipStream_t st, hipEvent_t* ev) {
   for (auto& m : c->marks)
     if (m.s == st) {
-      RT_HIP(hipEventRecord(m.ev, st));
+      *ev = m.ev;
       return RT_OK;
     }
   rt_ctx::Mark m{st, nullptr};
-  if (c->marks.size() >= 16) {        // many streams: the oldest mark's launches are waited for, its event reused
+  if (c->marks.size() >= 16) {
     m.ev = c->marks.front().ev;
     RT_HIP(hipEventSynchronize(m.ev));
     c->marks.erase(c->marks.begin());
@@ -54,7 +59,17 @@ int mark_launch(rt_ctx* c, hipStream_t st) {
     RT_HIP(hipEventCreateWithFlags(&m.ev, hipEventDisableTiming));
   }
   c->marks.push_back(m);
-  RT_HIP(hipEventRecord(m.ev, st));
+  *ev = m.ev;
+  return RT_OK;
+}
+
+int mark_launch(rt_ctx* c, hipStream_t st) {
+#ifdef RT_DIAG_NO_MARKS
+  return RT_OK;                       // diagnostic builds only: the marks' cost (A/B)
+#endif
+  hipEvent_t ev = nullptr;
+  RT_TRY(mark_event(c, st, &ev));
+  RT_HIP(hipEventRecord(ev, st));
   return RT_OK;
 }
 
@@ -247,11 +262,6 @@ int rt_ctx_set_option(rt_ctx* c, int32_t option, int32_t value) {
     rt::spec_drop(c);
     c->spec_on = value;
     if (c->uploaded) rt::spec_prepare(c, retry);   // a scene family registered since the upload may hold it
-    return RT_OK;
-  }
-  if (option == RT_OPT_TILES_PER_WAVE) {
-    if (value < 0 || value > 16) return fail(RT_ERR_INVALID, "RT_OPT_TILES_PER_WAVE %d not in [0, 16]", value);
-    c->tiles_per_wave = value;
     return RT_OK;
   }
   if (option == RT_OPT_WAVEFRONT_PAIRS) {

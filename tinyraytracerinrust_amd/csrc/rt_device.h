@@ -900,16 +900,41 @@ typedef LDS_AS double lds_f64;
 #define RT_LDS_RFRAMES 1
 #endif
 
+// The wave's frame POOL (KP > 0, chain and reflection-only kernels, round 5): instead of KL frames per
+// lane, the wave's LDS holds KP frame slots shared by its 64 lanes.  In those modes every hit spawns at
+// most one ray, so the lanes still walking push their frame f in the same iteration f: one ballot gives
+// the pushing lanes m, each takes slot start + (its rank in m) (mbcnt), and (m, start) are kept per f
+// (pool_mask / pool_start) so that a lane folding its frame f later finds its slot again.  Lanes whose
+// chains are short leave their share to the long ones: a spinning_globes wave needs ~2 frames per lane
+// on average but up to 10 for some lanes, so the fixed per-lane layout either spilled the deep frames
+// to scratch (KL = 5: 48.7 MB of HBM per 1080p frame) or cost occupancy.  Slots past KP, and frames of
+// pixels whose chain outgrows the pool, use the private array (scratch).  Layout at the wave's base lp:
+// [RT_MAX_DEPTH_CAP] u64 masks, [RT_MAX_DEPTH_CAP] u32 starts, then [4][KP] doubles (component-major:
+// the lanes of one push write consecutive doubles).
+constexpr int RT_POOL_HDR = RT_MAX_DEPTH_CAP + RT_MAX_DEPTH_CAP / 2;      // header doubles
+#define LDS_U64 __attribute__((address_space(3))) uint64_t
+#define LDS_U32 __attribute__((address_space(3))) uint32_t
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {                 // set lanes of m below this one
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // get_ray_color (raytracer.rs:132-287) for one primary ray, recursion unrolled onto a per-lane
 // frame stack.  REFR = the scene has a transparent object (refraction frames need more state).
 // KL > 0: frames 0..KL-1 of the stack are in LDS at lf[(f * 4 + c) * 64] (lf = this lane's slot);
 // KLR > 0 (REFR): the pending-reflection state of frames 0..KLR-1 at lf[(KL * 4 + f * 7 + c) * 64].
+// KP > 0 (not TREE, no recorder): the frames go to the wave's pool of KP slots at lp (above) instead.
 // CHAIN (REFR scenes with RtDevScene::ray_chains): every hit spawns at most one ray, so a refraction
 // frame never carries a pending reflection: frames are (A, w) as in the reflection-only kernels.
-template <bool REFR, class Rec = NoRec, int KL = 0, bool FC = false, int KLR = 0, bool CHAIN = false>
-RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, lds_f64* lf = nullptr) {
+template <bool REFR, class Rec = NoRec, int KL = 0, bool FC = false, int KLR = 0, bool CHAIN = false, int KP = 0>
+RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, lds_f64* lf = nullptr,
+                lds_f64* lp = nullptr) {
   double fA[RT_MAX_DEPTH_CAP][3];     // parent colour already intensified by (1 - w)
   double fW[RT_MAX_DEPTH_CAP];        // child weight w (transparency or reflectivity)
+  constexpr bool POOL = KP > 0 && !(REFR && !CHAIN) && same_type<Rec, NoRec>::value;
+  LDS_U64* const pool_mask = (LDS_U64*)lp;
+  LDS_U32* const pool_start = (LDS_U32*)(lp + RT_MAX_DEPTH_CAP);
+  lds_f64* const pool = lp + RT_POOL_HDR;
+  uint32_t pool_used = 0;             // wave-uniform: slots taken by the pushes so far
   auto put_frame = [&](int f, Col A, double w) {
     if (KL > 0 && f < KL) {
       lf[(f * 4 + 0) * 64] = A.r; lf[(f * 4 + 1) * 64] = A.g; lf[(f * 4 + 2) * 64] = A.b; lf[(f * 4 + 3) * 64] = w;
@@ -918,11 +943,34 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
     }
   };
   auto get_frame = [&](int f, Col* A, double* w) {
+    if constexpr (POOL) {
+      const uint32_t slot = pool_start[f] + lane_rank(pool_mask[f]);
+      if (slot < (uint32_t)KP) {
+        *A = {pool[slot], pool[KP + slot], pool[2 * KP + slot]}; *w = pool[3 * KP + slot];
+        return;
+      }
+    }
     if (KL > 0 && f < KL) {
       *A = {lf[(f * 4 + 0) * 64], lf[(f * 4 + 1) * 64], lf[(f * 4 + 2) * 64]}; *w = lf[(f * 4 + 3) * 64];
     } else {
       *A = {fA[f][0], fA[f][1], fA[f][2]}; *w = fW[f];
     }
+  };
+  // POOL: the frame every lane still walking pushes in this iteration (they are all at frame f)
+  auto pool_push = [&](bool push, int f, Col A, double w) {
+    const uint64_t m = __ballot(push);
+    const uint32_t start = pool_used;
+    if (push) {
+      const uint32_t slot = start + lane_rank(m);
+      if (slot < (uint32_t)KP) {
+        pool[slot] = A.r; pool[KP + slot] = A.g; pool[2 * KP + slot] = A.b; pool[3 * KP + slot] = w;
+      } else {
+        fA[f][0] = A.r; fA[f][1] = A.g; fA[f][2] = A.b; fW[f] = w;
+      }
+      pool_mask[f] = m;                 // every pushing lane writes the same (m, start)
+      pool_start[f] = start;
+    }
+    pool_used = start + (uint32_t)__builtin_popcountll(m);
   };
   constexpr bool TREE = REFR && !CHAIN;       // a hit may spawn two rays: pending reflections
   double fP[TREE ? RT_MAX_DEPTH_CAP : 1][3], fD[TREE ? RT_MAX_DEPTH_CAP : 1][3];
@@ -956,8 +1004,11 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
   [[maybe_unused]] int ray_type = 0, slot = 0;                  // RayType::NormalRay
   int sp = 0, depth = 0;
   Col C = {0.0, 0.0, 0.0};
-  for (;;) {
+  for (int iter = 0;; ++iter) {
     bool descend = false;
+    [[maybe_unused]] bool pushing = false;        // POOL: this lane pushes frame `iter` (its sp) now
+    [[maybe_unused]] Col push_A = {0.0, 0.0, 0.0};
+    [[maybe_unused]] double push_w = 0.0;
     double t_hit;
     int oi;
     oi = nearest_hit<SHARE, OBB>(S, ro, rd, &t_hit);
@@ -1020,8 +1071,17 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
       if (do_refr) tdir = refract_dir(rd, n2, r1 / r2, &tir);
       const double rp = tir ? refl + (1.0 - refl) * transp : refl;       // :261-265
       const bool do_refl = depth < max_depth && rp != 0.0 && (!inside || tir);   // :267
+      if constexpr (POOL) {             // one push point for both kinds of child (see pool_push)
+        const bool rfr = do_refr && !tir;
+        if (rfr || do_refl) {
+          const double w = rfr ? transp : rp;
+          push_A = intensify<FC>(L, 1.0 - w);
+          push_w = w;
+          pushing = true;
+        }
+      }
       if (do_refr && !tir) {
-        put_frame(sp, intensify<FC>(L, 1.0 - transp), transp);
+        if constexpr (!POOL) put_frame(sp, intensify<FC>(L, 1.0 - transp), transp);
         if constexpr (TREE) {
           pend = do_refl ? pend | (1u << sp) : pend & ~(1u << sp);
           if (do_refl) put_rframe(sp, p, reflect_dir(rd, n2), rp);
@@ -1033,7 +1093,7 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
         depth = sp;
         descend = true;
       } else if (do_refl) {
-        put_frame(sp, intensify<FC>(L, 1.0 - rp), rp);
+        if constexpr (!POOL) put_frame(sp, intensify<FC>(L, 1.0 - rp), rp);
         if constexpr (TREE) pend &= ~(1u << sp);
         if constexpr (RECORD) { fSlot[sp] = slot; ray_type = 1; }        // ReflectionRay
         ++sp;
@@ -1046,6 +1106,7 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
       }
     }
     if constexpr (RECORD) { if (!descend) rec->finish(slot, C); }     // leaf ray (or miss) reports now
+    if constexpr (POOL) pool_push(pushing, iter, push_A, push_w);        // frame `iter` (= sp before the push)
     if (descend) continue;
     while (sp > 0) {                                                      // post-order combine
       const int f = sp - 1;
@@ -1354,16 +1415,30 @@ __device__ __forceinline__ void store_pixel(uint8_t* row, int x, Col c, int rgb)
 // instantiation) is the only one that carries the timing code.
 // KL_ >= 0: that many stack frames in LDS (the specialised kernels at 4 waves/SIMD have room for more).
 // rows_entry: entry `entry` of the launch (a tile index, or the order's entry-th tile); rows_body: the
-// workgroup's own entry (blockIdx.x).  The specialised kernels may loop a wave over several entries
-// (spec.hip, RT_OPT_TILES_PER_WAVE: cheap launches whose waves are too short to amortise their dispatch).
-template <int MODE, bool F64, bool CAL, bool FC, int KL_ = -1>
+// workgroup's own entry (blockIdx.x).  (A wave looping over several entries grid-stride was measured
+// and lost: the loop's live state cost the megakernels 6 more spilled VGPRs, profiles/r07c_tiles_per_wave.txt.)
+// The row kernels' frame storage per one-wave workgroup: the reflection-only and chain modes take a
+// wave pool (trace(), KP slots) by default; KL_ >= 0 asks for KL_ frames per lane instead (the round-4
+// layout, diagnostic A/B); KP_ >= 0 sets the pool's size.  The ray-tree mode keeps per-lane frames.
+#ifndef RT_LDS_POOL_REFL
+#define RT_LDS_POOL_REFL 122        // 4 KB per workgroup, the space of the per-lane KL = 2 frames
+#endif
+#ifndef RT_LDS_POOL_CHAIN
+#define RT_LDS_POOL_CHAIN 186       // 6 KB: 26 workgroups per CU, so the VGPRs set the occupancy (5-6 waves/SIMD)
+#endif
+template <int MODE, int KL_ = -1, int KP_ = -1>
+constexpr int rows_pool_slots() {
+  return KL_ >= 0 || MODE == RT_MODE_TREE ? 0 : KP_ >= 0 ? KP_ : MODE == RT_MODE_CHAIN ? RT_LDS_POOL_CHAIN : RT_LDS_POOL_REFL;
+}
+template <int MODE, bool F64, bool CAL, bool FC, int KL_ = -1, int KP_ = -1>
 __device__ __forceinline__ void rows_entry(const RtDevScene& S, unsigned entry, int y_first, int band_rows, int band_pitch,
                                            int n_rows, int max_depth, uint8_t* __restrict__ out, size_t stride,
                                            const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb,
                                            lds_f64* frames) {
   constexpr bool REFR = MODE != RT_MODE_REFL, CHAIN = MODE == RT_MODE_CHAIN;
   constexpr int KLR = MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0;
-  constexpr int KL = KL_ >= 0 ? KL_ : CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES;
+  constexpr int KP = rows_pool_slots<MODE, KL_, KP_>();
+  constexpr int KL = KP > 0 ? 0 : KL_ >= 0 ? KL_ : CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES;
   const int lane = threadIdx.x & 63;
   const unsigned tile = CAL || !order ? entry : (unsigned)order[entry];
   [[maybe_unused]] uint64_t t_start = 0;
@@ -1375,23 +1450,25 @@ __device__ __forceinline__ void rows_entry(const RtDevScene& S, unsigned entry, 
   if (y >= S.height) return;
   V3 ro, rd;
   camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
-  const Col c = trace<REFR, NoRec, KL, FC, KLR, CHAIN>(make_ds(S), ro, rd, max_depth, nullptr, frames + lane);
+  const Col c = trace<REFR, NoRec, KL, FC, KLR, CHAIN, KP>(make_ds(S), ro, rd, max_depth, nullptr, frames + lane, frames);
   store_pixel<F64>(out + (size_t)r * stride, x, c, rgb);
   if constexpr (CAL)
     if (threadIdx.x == 0) cost[tile] = (uint32_t)(wall_clock64() - t_start);   // vector store
 }
-template <int MODE, bool F64, bool CAL, bool FC, int KL_ = -1>
+template <int MODE, bool F64, bool CAL, bool FC, int KL_ = -1, int KP_ = -1>
 __device__ __forceinline__ void rows_body(const RtDevScene& S, int y_first, int band_rows, int band_pitch, int n_rows,
                                           int max_depth, uint8_t* __restrict__ out, size_t stride,
                                           const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb,
                                           lds_f64* frames) {
-  rows_entry<MODE, F64, CAL, FC, KL_>(S, blockIdx.x, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, order,
-                                      cost, rgb, frames);
+  rows_entry<MODE, F64, CAL, FC, KL_, KP_>(S, blockIdx.x, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride,
+                                           order, cost, rgb, frames);
 }
-template <int MODE, int KL_ = -1>
+template <int MODE, int KL_ = -1, int KP_ = -1>
 constexpr int rows_lds_doubles() {
-  return ((KL_ >= 0 ? KL_ : MODE == RT_MODE_CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES) * 4 +
-          (MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0) * 7) * 64;
+  return rows_pool_slots<MODE, KL_, KP_>() > 0
+             ? RT_POOL_HDR + 4 * rows_pool_slots<MODE, KL_, KP_>()
+             : ((KL_ >= 0 ? KL_ : MODE == RT_MODE_CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES) * 4 +
+                (MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0) * 7) * 64;
 }
 
 // The deferred-shadow kernel's body (reflection-only scenes, or refraction chains on request): one

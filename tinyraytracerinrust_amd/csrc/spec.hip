@@ -288,22 +288,23 @@ static std::string spec_kernel(int kind, int mode, bool fc, int f64, int cal) {
   // stack frames in LDS: 4 waves/SIMD leave 10 KB per one-wave workgroup (the generic kernel's 2
   // frames at 5 waves: 4 KB); RT_SPEC_LDS_FRAMES (diagnostic builds) overrides the mode's default
 #ifdef RT_SPEC_LDS_FRAMES
-  const int kl = RT_SPEC_LDS_FRAMES;
+  int kl = RT_SPEC_LDS_FRAMES;
 #else
-  const int kl = -1;
+  int kl = -1;
 #endif
-  // the megakernel takes its entries grid-stride: entry blockIdx.x, + gridDim.x, ... < n_entries (launch_bands
-  // launches n_entries / tiles-per-wave workgroups for cheap launches; one entry per wave otherwise)
+  int kp = -1;                                                  // the wave pool's slots (-1: the mode's default)
+#ifdef RT_DIAG_ENV
+  if (const char* e = getenv("RT_SPEC_KL")) kl = atoi(e);      // diagnostic builds: A/B of the LDS frames
+  if (const char* e = getenv("RT_SPEC_KP")) kp = atoi(e);
+#endif
   if (kind == 0)
     snprintf(buf, sizeof buf,
              "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(%s))) "
-             "void rt_spec_rows_%d%d(RtDevScene S, int y_first, int band_rows, int band_pitch, int n_rows, int max_depth, "
-             "uint8_t* __restrict__ out, size_t stride, const int32_t* __restrict__ order, uint32_t* __restrict__ cost, "
-             "int rgb, unsigned n_entries) {\n  __shared__ double s_frames[rows_lds_doubles<%d, %d>()];\n"
-             "  for (unsigned e = blockIdx.x; e < n_entries; e += gridDim.x)\n"
-             "    rows_entry<%d, %s, %s, %s, %d>(S, e, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, order, "
+             "void rt_spec_rows_%d%d%s {\n  __shared__ double s_frames[rows_lds_doubles<%d, %d, %d>()];\n"
+             "  rows_body<%d, %s, %s, %s, %d, %d>(S, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride, order, "
              "cost, rgb, (lds_f64*)s_frames);\n}\n",
-             waves, f64, cal, mode, kl, mode, f64 ? "true" : "false", cal ? "true" : "false", fc ? "true" : "false", kl);
+             waves, f64, cal, args, mode, kl, kp, mode, f64 ? "true" : "false", cal ? "true" : "false", fc ? "true" : "false",
+             kl, kp);
   else
     snprintf(buf, sizeof buf,
              "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_DEFERRED))) "
@@ -544,7 +545,7 @@ int spec_compile(const std::string& src, SpecCode* out, std::string* err) {
 
 int spec_guard(const SpecCode& c, const std::string& text, std::string* err) {
   const bool def = c.name.rfind("rt_spec_def_", 0) == 0;
-  const bool tree = text.find("rows_entry<" + std::to_string(RT_MODE_TREE) + ",") != std::string::npos;
+  const bool tree = text.find("rows_body<" + std::to_string(RT_MODE_TREE) + ",") != std::string::npos;
   const int max_scratch = def ? RT_SPEC_MAX_SCRATCH_DEF : tree ? RT_SPEC_MAX_SCRATCH_TREE : RT_SPEC_MAX_SCRATCH_ROWS;
   if (c.name.empty() || c.vgprs < 0 || c.scratch < 0) {
     *err = "resource guard: the code object's metadata holds no resource usage for the kernel";
