@@ -272,9 +272,11 @@ int rt_ctx_synchronize(rt_ctx* ctx);
  * sorted by object, so a wave tests one object against 64 rays (wfp_* kernels; scenes whose shadow
  * products are order-free, RtDevScene::shadow_pow, and fewer than 4096 objects; else as 0); 2 level 0
  * (the camera rays) too.  The wavefront path synchronises the host with the launch stream once per
- * recursion level (it reads each level's ray count), and RT_KERNEL_AUTO's first ordered launch of a
- * ray-tree geometry times one wavefront launch against the megakernel (blocking, once): such
- * launches return only after the work is done, even with device output.
+ * launch on the pair path (its levels read their ray counts on the device; the host checks the pair
+ * lists' capacity at the end) and once per recursion level on the wave walk (it reads each level's ray
+ * count), and RT_KERNEL_AUTO's first ordered launch of a ray-tree geometry times one wavefront launch
+ * against the megakernel (blocking, once): such launches return only after the work is done, even with
+ * device output.
  * RT_OPT_SPECIALIZE: 1 (default) compiles the uploaded scene's row kernels once more with the scene's
  * tables as constants (hipRTC, spec.hip: the hierarchy walk unrolled, every record field a literal;
  * same pixels) for RGBA8 / RGB8 launches; 2 for the f64 and calibration launches too; 0 never.  The

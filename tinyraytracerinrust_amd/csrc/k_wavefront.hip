@@ -257,9 +257,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER
 }
 
 template <bool F64, bool FC>
-__global__ __launch_bounds__(256) void wf_fold_kernel(RtDevScene S, WfArena A, int d, uint32_t n, int y_first,
-                                                      int band_rows, int band_pitch, int n_rows,
+__global__ __launch_bounds__(256) void wf_fold_kernel(RtDevScene S, WfArena A, int d, uint32_t n, const uint32_t* n_dev,
+                                                      int y_first, int band_rows, int band_pitch, int n_rows,
                                                       uint8_t* __restrict__ out, size_t stride, int rgb) {
+  if (n_dev) n = min(*n_dev, A.cap);                         // a device-driven level's count
   const WfLevel lv = wf_level(A, d);
   const WfLevel ch = wf_level(A, d + 1);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -365,7 +366,7 @@ struct WfPairs {
 constexpr unsigned long long RT_WFP_NONE = 0x7FF0000000000000ull;   // +inf
 constexpr int RT_WFP_COUNT = 32;      // the pair counts' words in WfArena::count (after the level counts)
 static_assert(RT_MAX_DEPTH_CAP + 3 <= RT_WFP_COUNT, "wavefront counter block");
-static_assert(RT_WFP_COUNT + 3 <= 64, "wavefront counter block: 256 bytes");
+static_assert(RT_WFP_COUNT + 5 <= 64, "wavefront counter block: 256 bytes");
 
 // The object's nearest accepted distance for one ray: nearest_hit's body for one object, its best
 // starting at +inf (the leaf boxes' tmax only shrinks, as share_prev requires).
@@ -448,17 +449,22 @@ __device__ __forceinline__ bool wf_get_ray(const RtDevScene& S, const WfLevel& l
 // the hierarchy into LDS and the walks read it there.
 constexpr int RT_WFP_CAND_WAVES = 4;
 constexpr uint32_t RT_WFP_LDS_TRAV_MAX = 640;     // nodes (40 KB) staged at most; larger: global loads
+// n_dev != nullptr (device-driven levels): the level's ray count is min(*n_dev, A.cap), read here; the
+// grid is then a fixed number of workgroups that take the level's rays grid-stride, 64 x WG_WAVES at a
+// time (the hierarchy staged in LDS once per workgroup).
 template <bool SHADOW, bool LDS_TRAV>
 __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevScene S, WfArena A, WfPairs P, int d,
-                                                                          uint32_t n, int y_first, int band_rows,
-                                                                          int band_pitch, int n_rows) {
+                                                                          uint32_t n, const uint32_t* n_dev,
+                                                                          int y_first, int band_rows, int band_pitch,
+                                                                          int n_rows) {
   constexpr int WW = LDS_TRAV ? RT_WFP_CAND_WAVES : 1;
   __shared__ uint32_t sk_all[WW][RT_WFP_BUF], sv_all[WW][RT_WFP_BUF];
   extern __shared__ __attribute__((aligned(16))) uint8_t s_trav[];
   const int lane = threadIdx.x & 63, wv = (int)(threadIdx.x >> 6);
   uint32_t* sk = sk_all[LDS_TRAV ? wv : 0];
   uint32_t* sv = sv_all[LDS_TRAV ? wv : 0];
-  const uint32_t i = blockIdx.x * (64u * WW) + threadIdx.x;
+  if (n_dev) n = min(*n_dev, A.cap);
+  if (blockIdx.x * (64u * WW) >= n) return;                  // no ray for this workgroup: no staging either
   if constexpr (LDS_TRAV) {                                   // the hierarchy into LDS, once per workgroup
     const uint4* g = (const uint4*)S.trav;
     uint4* l = (uint4*)s_trav;
@@ -467,13 +473,6 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
   }
   const WfLevel lv = wf_level(A, d);
   const DS D = make_ds(S);
-  bool live = i < n;
-  uint32_t j = i;
-  V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
-  if (live) {
-    j = SHADOW ? P.hperm[i] : (d > 0 && A.perm) ? A.perm[i] : i;
-    if (!SHADOW) live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
-  }
   uint32_t nb = 0;                                           // wave-uniform fill of the LDS buffer
   auto wave_sync = []() {                                    // the wave's own buffer: a wave-level barrier
     if constexpr (LDS_TRAV) {
@@ -532,45 +531,55 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
       emit(h, (uint32_t)ob, id);
     }
   };
-  if constexpr (!SHADOW) {
-    if (i < n) { P.tmin[j] = RT_WFP_NONE; P.omin[j] = 0x7fffffff; }   // slots outside the frame too
-    // A bound on the nearest hit: the object whose hit spawned the ray, evaluated first (a ray that
-    // refracted into or reflects inside a closed shape meets it again).  The walk then tests boxes
-    // against [0, cull_tmax(bound)] only -- conservative, as nearest_hit's running best is; the
-    // parent's own pair is still emitted by the walk (its box contains the bound's point).
-    double bound = INFINITY;
-    if (d > 0) {
-      const int32_t par = live ? lv.par[j] : -1;
-      const CullRay cr = cull_ray(ro, rd);
-      uint64_t todo = __ballot(live && par >= 0);
-      while (todo) {                     // the children of one shading wave: mostly one parent
-        const int pu = __builtin_amdgcn_readlane(par, (int)__builtin_ctzll(todo));
-        const uint64_t mine = __ballot(live && par == pu);
-        todo &= ~mine;
-        if ((mine >> lane) & 1) bound = wfp_object_nearest(D, pu, ro, rd, cr);
-      }
+  for (uint32_t base = blockIdx.x * (64u * WW); base < n; base += gridDim.x * (64u * WW)) {   // wave-uniform
+    const uint32_t i = base + threadIdx.x;
+    bool live = i < n;
+    uint32_t j = i;
+    V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
+    if (live) {
+      j = SHADOW ? P.hperm[i] : (d > 0 && A.perm) ? A.perm[i] : i;
+      if (!SHADOW) live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
     }
-    walk(live, ro, rd, bound < INFINITY ? cull_tmax(bound) : INFINITY, j);
-  } else {
-    const int32_t oi = live ? P.omin[j] : 0x7fffffff;
-    const bool hit = live && oi != 0x7fffffff;
-    V3 p = {0.0, 0.0, 0.0};
-    if (hit) p = {P.px[j], P.py[j], P.pz[j]};                     // wfp_hit_key_kernel
-    for (int k = 0; k < D.n_lights; ++k) {
-      V3 sdir = {0.0, 0.0, 0.0};
-      double tmax = 0.0;
-      const uint32_t s = j * (uint32_t)D.n_lights + (uint32_t)k;
-      if (hit) {
-        cptr<RtLight> lt = &D.lights[k];
-        const V3 l = sub(ld3(lt->p), p);
-        double ll, ill;
-        len_inv(l, &ll, &ill);
-        sdir = scale(l, ill);
-        tmax = cull_tmax(ll);
-        P.kcnt[s] = 0;
-        P.opq[s] = 0;
+    if constexpr (!SHADOW) {
+      if (i < n) { P.tmin[j] = RT_WFP_NONE; P.omin[j] = 0x7fffffff; }   // slots outside the frame too
+      // A bound on the nearest hit: the object whose hit spawned the ray, evaluated first (a ray that
+      // refracted into or reflects inside a closed shape meets it again).  The walk then tests boxes
+      // against [0, cull_tmax(bound)] only -- conservative, as nearest_hit's running best is; the
+      // parent's own pair is still emitted by the walk (its box contains the bound's point).
+      double bound = INFINITY;
+      if (d > 0) {
+        const int32_t par = live ? lv.par[j] : -1;
+        const CullRay cr = cull_ray(ro, rd);
+        uint64_t todo = __ballot(live && par >= 0);
+        while (todo) {                     // the children of one shading wave: mostly one parent
+          const int pu = __builtin_amdgcn_readlane(par, (int)__builtin_ctzll(todo));
+          const uint64_t mine = __ballot(live && par == pu);
+          todo &= ~mine;
+          if ((mine >> lane) & 1) bound = wfp_object_nearest(D, pu, ro, rd, cr);
+        }
       }
-      walk(hit, p, sdir, tmax, s);
+      walk(live, ro, rd, bound < INFINITY ? cull_tmax(bound) : INFINITY, j);
+    } else {
+      const int32_t oi = live ? P.omin[j] : 0x7fffffff;
+      const bool hit = live && oi != 0x7fffffff;
+      V3 p = {0.0, 0.0, 0.0};
+      if (hit) p = {P.px[j], P.py[j], P.pz[j]};                     // wfp_hit_key_kernel
+      for (int k = 0; k < D.n_lights; ++k) {
+        V3 sdir = {0.0, 0.0, 0.0};
+        double tmax = 0.0;
+        const uint32_t s = j * (uint32_t)D.n_lights + (uint32_t)k;
+        if (hit) {
+          cptr<RtLight> lt = &D.lights[k];
+          const V3 l = sub(ld3(lt->p), p);
+          double ll, ill;
+          len_inv(l, &ll, &ill);
+          sdir = scale(l, ill);
+          tmax = cull_tmax(ll);
+          P.kcnt[s] = 0;
+          P.opq[s] = 0;
+        }
+        walk(hit, p, sdir, tmax, s);
+      }
     }
   }
   flush();
@@ -625,8 +634,9 @@ __global__ __launch_bounds__(256) void wfp_near_tie_kernel(WfPairs P) {
 // of the hit point's cell (a wave then shades one object -- shade_inputs' waterfall runs once -- and
 // its shadow rays start close together); misses sort last.
 __global__ __launch_bounds__(256) void wfp_hit_key_kernel(RtDevScene S, WfArena A, WfPairs P, int d, uint32_t n,
-                                                          int y_first, int band_rows, int band_pitch, int n_rows,
-                                                          int cbits) {
+                                                          const uint32_t* n_dev, int y_first, int band_rows,
+                                                          int band_pitch, int n_rows, int cbits) {
+  if (n_dev) n = min(*n_dev, A.cap);
   const WfLevel lv = wf_level(A, d);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t j = (d > 0 && A.perm) ? A.perm[i] : i;
@@ -681,12 +691,9 @@ __global__ __launch_bounds__(64) void wfp_shadow_eval_kernel(RtDevScene S, WfPai
 }
 
 template <bool REFR, bool FC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_WF))) void wfp_shade_kernel(
-    RtDevScene S, WfArena A, WfPairs P, int d, uint32_t n, int y_first, int band_rows, int band_pitch, int n_rows,
-    int max_depth) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
-  const WfLevel lv = wf_level(A, d);
+__device__ __forceinline__ void wfp_shade_one(RtDevScene S, WfArena A, WfPairs P, const WfLevel& lv, int d, uint32_t i,
+                                              uint32_t n, int lane, int y_first, int band_rows, int band_pitch,
+                                              int n_rows, int max_depth) {
   bool live = i < n;
   V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
   uint32_t j = i;
@@ -723,6 +730,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER
         },
         &L, &wt, &wr, &ch_t, &ch_r, &p, &dt, &dr);
   wf_append(A, lv, d, lane, live, j, pix, L, wt, wr, ch_t, ch_r, p, dt, dr, live ? P.omin[j] : -1);
+}
+
+
+// End of a device-driven pair level: its pair counts against the arena (a level that emitted more pairs
+// than the lists hold computed wrong nearest hits), kept in sticky words the host reads once per launch:
+// count[RT_WFP_COUNT + 3] = the most pairs any level emitted beyond the capacity, [+ 4] = a count wrapped.
+__global__ void wfp_level_check_kernel(uint32_t* count, uint32_t cap);
+
+// n_dev != nullptr (device-driven levels): the ray count is min(*n_dev, A.cap); the waves take the
+// level's rays grid-stride, 64 at a time (wf_append: one ballot + one atomic per wave and chunk).
+template <bool REFR, bool FC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_WF))) void wfp_shade_kernel(
+    RtDevScene S, WfArena A, WfPairs P, int d, uint32_t n, const uint32_t* n_dev, int y_first, int band_rows,
+    int band_pitch, int n_rows, int max_depth) {
+  const int lane = threadIdx.x & 63;
+  if (n_dev) n = min(*n_dev, A.cap);
+  const WfLevel lv = wf_level(A, d);
+  for (uint32_t base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u)   // wave-uniform
+    wfp_shade_one<REFR, FC>(S, A, P, lv, d, base + (uint32_t)lane, n, lane, y_first, band_rows, band_pitch, n_rows,
+                            max_depth);
+}
+
+__global__ void wfp_level_check_kernel(uint32_t* count, uint32_t cap) {
+  const uint32_t* pc = count + RT_WFP_COUNT;
+  const uint32_t m = max(pc[0], pc[1]);
+  if (m > cap) atomicMax(count + RT_WFP_COUNT + 3, m);
+  if (pc[2]) atomicOr(count + RT_WFP_COUNT + 4, 1u);
 }
 
 }  // namespace
@@ -794,73 +828,67 @@ static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t lcap, size_t ne
 
 // One level of the wavefront path through the pair path: candidate pairs, sort by object, pair
 // evaluation and the folds, for the nearest hits and then the shadow rays, then the shading pass.
-// The pair counts stay on the device (the sorts and the evaluation kernels read them; their grids
-// are sized for the arena), so a level costs ONE host synchronisation, at its end: it reads the next
-// level's ray count and both pair counts.  A pair count beyond the arena grows it and runs the level
-// again (the level's outputs are recomputed from its rays; level d + 1 is refilled from empty).
-static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int d, uint32_t n, int a0, int a1,
-                     int a2, int a3, int max_depth, bool refr, bool fc, uint32_t* next) {
+// Device-driven (round 5): no host synchronisation.  The level's ray count is n (known on the host:
+// level 0) or min(A.count[d], cap), read by the kernels themselves (n_dev); the pair counts stay on the
+// device too (the sorts and the evaluations read them).  Grids are fixed and the kernels take their
+// work grid-stride, so the host launches every level back to back.  A level whose pairs outgrew the
+// lists leaves the sticky overflow word (wfp_level_check_kernel); the host reads it once, after the
+// whole launch, and renders the launch again with lists of that size (launch_wavefront).
+static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int d, uint32_t n_ub, const uint32_t* n_dev,
+                     int a0, int a1, int a2, int a3, int max_depth, bool refr, bool fc) {
   WfPairs P;
   int rc = wfp_arena(c, st, R, A.cap, 0, &P);
   if (rc) return rc;
   P.count = A.count + RT_WFP_COUNT;
-  const dim3 g((n + 63) / 64), b64(64);
+  const uint32_t ncu = (uint32_t)c->n_cu;
+  auto grid = [&](uint32_t per_wg, uint32_t max_wg) { return dim3(std::max(1u, std::min((n_ub + per_wg - 1) / per_wg, max_wg))); };
+  const dim3 b64(64);
   const uint32_t nobj = (uint32_t)c->dev.n_objects;
   uint32_t* bins[3] = {P.bins, P.bins + 4096, P.bins + 8192};
   // the candidate walks: hierarchies of up to RT_WFP_LDS_TRAV_MAX nodes staged in LDS (4-wave groups)
   const bool lds_trav = (uint32_t)c->dev.n_trav <= RT_WFP_LDS_TRAV_MAX && !diag_env("RT_WFP_GLOBAL_TRAV");
   auto launch_cand = [&](bool shadow) {
     if (lds_trav) {
-      const dim3 gl((n + 64 * RT_WFP_CAND_WAVES - 1) / (64 * RT_WFP_CAND_WAVES)), bl(64 * RT_WFP_CAND_WAVES);
+      const dim3 gl = grid(64 * RT_WFP_CAND_WAVES, ncu * 16), bl(64 * RT_WFP_CAND_WAVES);
       const size_t lds = (size_t)c->dev.n_trav * sizeof(RtTrav);
-      if (shadow) hipLaunchKernelGGL((wfp_cand_kernel<true, true>), gl, bl, lds, st, c->dev, A, P, d, n, a0, a1, a2, a3);
-      else hipLaunchKernelGGL((wfp_cand_kernel<false, true>), gl, bl, lds, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+      if (shadow) hipLaunchKernelGGL((wfp_cand_kernel<true, true>), gl, bl, lds, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3);
+      else hipLaunchKernelGGL((wfp_cand_kernel<false, true>), gl, bl, lds, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3);
     } else if (shadow) {
-      hipLaunchKernelGGL((wfp_cand_kernel<true, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+      hipLaunchKernelGGL((wfp_cand_kernel<true, false>), grid(64, ncu * 64), b64, 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1,
+                         a2, a3);
     } else {
-      hipLaunchKernelGGL((wfp_cand_kernel<false, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3);
+      hipLaunchKernelGGL((wfp_cand_kernel<false, false>), grid(64, ncu * 64), b64, 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1,
+                         a2, a3);
     }
   };
-  for (;;) {
-    // grid-stride evaluations: one pass covers ~4 pairs per ray of the level (fractal: ~3), capped at
-    // 8 waves per SIMD -- small levels then launch hundreds, not thousands, of idle workgroups
-    const dim3 ge(std::max<uint32_t>((uint32_t)c->n_cu, std::min<uint32_t>((uint32_t)(((size_t)n * 4 + 63) / 64),
-                                                                          (uint32_t)c->n_cu * 32u)));
-    RT_HIP(hipMemsetAsync(P.count, 0, 12, st));
-    RT_HIP(hipMemsetAsync(P.bins, 0, 3 * 16384, st));        // the three sorts' bucket counters
-    launch_cand(false);
-    RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count, nobj, 0, bins[0], false, st));
-    hipLaunchKernelGGL(wfp_near_eval_kernel, ge, b64, 0, st, c->dev, A, P, d, a0, a1, a2, a3);
-    hipLaunchKernelGGL(wfp_near_tie_kernel, dim3(std::min<uint32_t>((P.cap + 255) / 256, 4096)), dim3(256), 0, st, P);
-    // the hit points and their order for the shadow and shading passes: at most 4096 buckets of
-    // (hit object, coarse hit-point cell), unordered within a bucket (a 16^3-cell-only key and the
-    // full 27-bit radix sort measured slower: profiles/r03o_sort_ab.txt, r03w_*)
-    int cbits = 0;
-    while (cbits < 12 && ((nobj + 1u) << (cbits + 1)) <= 4096u) ++cbits;
-    hipLaunchKernelGGL(wfp_hit_key_kernel, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, st, c->dev,
-                       A, P, d, n, a0, a1, a2, a3, cbits);
-    RT_HIP(rt_wf_bucket_sort(P.hkey, P.hkey_s, P.hval, P.hperm, n, nullptr, (nobj + 1u) << cbits, 0, bins[1], false, st));
-    launch_cand(true);
-    RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count + 1, nobj, 0, bins[2], false, st));
-    hipLaunchKernelGGL(wfp_shadow_eval_kernel, ge, b64, 0, st, c->dev, P);
-    if (refr && fc) hipLaunchKernelGGL((wfp_shade_kernel<true, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
-    else if (refr) hipLaunchKernelGGL((wfp_shade_kernel<true, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
-    else if (fc) hipLaunchKernelGGL((wfp_shade_kernel<false, true>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
-    else hipLaunchKernelGGL((wfp_shade_kernel<false, false>), g, b64, 0, st, c->dev, A, P, d, n, a0, a1, a2, a3, max_depth);
-    RT_HIP(hipGetLastError());
-    uint32_t cb[RT_WFP_COUNT + 3];        // the whole counter block in one copy: level counts, pair counts, wrap flag
-    RT_HIP(hipMemcpyAsync(cb, A.count, sizeof cb, hipMemcpyDeviceToHost, st));
-    RT_HIP(hipStreamSynchronize(st));
-    if (cb[RT_WFP_COUNT + 2]) return fail(RT_ERR_UNSUPPORTED, "wavefront pair count of level %d passed 2^31", d);
-    *next = d < max_depth ? cb[d + 1] : 0u;
-    const uint32_t pc[2] = {cb[RT_WFP_COUNT], cb[RT_WFP_COUNT + 1]};
-    if (pc[0] <= P.cap && pc[1] <= P.cap) return RT_OK;
-    rc = wfp_arena(c, st, R, A.cap, std::max(pc[0], pc[1]), &P);   // grow (synchronises), then this level again
-    if (rc) return rc;
-    P.count = A.count + RT_WFP_COUNT;
-    bins[0] = P.bins; bins[1] = P.bins + 4096; bins[2] = P.bins + 8192;
-    if (d < max_depth) RT_HIP(hipMemsetAsync(A.count + d + 1, 0, 4, st));
-  }
+  // grid-stride evaluations: one pass covers ~4 pairs per ray of the level (fractal: ~3), at most 8
+  // waves per SIMD
+  const dim3 ge(std::max<uint32_t>(ncu, std::min<uint32_t>((uint32_t)(((size_t)n_ub * 4 + 63) / 64), ncu * 32u)));
+  RT_HIP(hipMemsetAsync(P.count, 0, 12, st));
+  RT_HIP(hipMemsetAsync(P.bins, 0, 3 * 16384, st));        // the three sorts' bucket counters
+  launch_cand(false);
+  RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count, nobj, 0, bins[0], false, st));
+  hipLaunchKernelGGL(wfp_near_eval_kernel, ge, b64, 0, st, c->dev, A, P, d, a0, a1, a2, a3);
+  hipLaunchKernelGGL(wfp_near_tie_kernel, dim3(std::min<uint32_t>((P.cap + 255) / 256, 4096)), dim3(256), 0, st, P);
+  // the hit points and their order for the shadow and shading passes: at most 4096 buckets of
+  // (hit object, coarse hit-point cell), unordered within a bucket (a 16^3-cell-only key and the
+  // full 27-bit radix sort measured slower: profiles/r03o_sort_ab.txt, r03w_*)
+  int cbits = 0;
+  while (cbits < 12 && ((nobj + 1u) << (cbits + 1)) <= 4096u) ++cbits;
+  hipLaunchKernelGGL(wfp_hit_key_kernel, grid(256, ncu * 8), dim3(256), 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3,
+                     cbits);
+  RT_HIP(rt_wf_bucket_sort(P.hkey, P.hkey_s, P.hval, P.hperm, n_ub, n_dev, (nobj + 1u) << cbits, 0, bins[1], false, st));
+  launch_cand(true);
+  RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count + 1, nobj, 0, bins[2], false, st));
+  hipLaunchKernelGGL(wfp_shadow_eval_kernel, ge, b64, 0, st, c->dev, P);
+  const dim3 gs = grid(64, ncu * 32);
+  if (refr && fc) hipLaunchKernelGGL((wfp_shade_kernel<true, true>), gs, b64, 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3, max_depth);
+  else if (refr) hipLaunchKernelGGL((wfp_shade_kernel<true, false>), gs, b64, 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3, max_depth);
+  else if (fc) hipLaunchKernelGGL((wfp_shade_kernel<false, true>), gs, b64, 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3, max_depth);
+  else hipLaunchKernelGGL((wfp_shade_kernel<false, false>), gs, b64, 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3, max_depth);
+  hipLaunchKernelGGL(wfp_level_check_kernel, dim3(1), dim3(1), 0, st, A.count, P.cap);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
 }
 
 // The wavefront path (wf_*_kernel): level 0 (the pixel slots), then each level the previous one
@@ -868,7 +896,7 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
 // fix-up.  The host reads every level's ray count (one stream synchronisation per level) to launch
 // exactly one wave per 64 rays and to stop at the first empty level.
 int rt::launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int a3, int max_depth, uint8_t* target,
-                            size_t tstride, bool f64, int rgbi, size_t n_tiles) {
+                            size_t tstride, bool f64, int rgbi, size_t n_tiles, int retry) {
   const size_t slots = n_tiles * 64, cap = std::max<size_t>(64, (slots * (size_t)c->wf_cap_pct / 100 + 63) & ~(size_t)63);
   if (cap > 0x7fffffffull || slots > 0x7fffffffull) return fail(RT_ERR_UNSUPPORTED, "wavefront launch of %zu pixel slots too large", slots);
   // the non-pair levels' coherence order: the in-tree bucket sort on the key's top 12 bits (direction
@@ -913,57 +941,61 @@ int rt::launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int 
   const bool pairs = c->wf_pairs > 0 && c->dev.shadow_pow != 0 && c->dev.n_objects > 0 && c->dev.n_objects < 4096 &&
                      (uint64_t)std::max(slots, cap) * (uint64_t)std::max(1, c->dev.n_lights) < (1ull << 32);
   auto pairs_level = [&](int d) { return pairs && (d > 0 || c->wf_pairs == 2); };
+  // n_level[d]: the level's ray count when the host knows it (level 0, and levels the wave walk traced,
+  // whose count it reads); known[d] = false: a device-driven pair level (its kernels read A.count[d])
   uint32_t n_level[RT_MAX_DEPTH_CAP + 2] = {0};
+  bool known[RT_MAX_DEPTH_CAP + 2] = {false};
   n_level[0] = (uint32_t)slots;
+  known[0] = true;
+  bool any_pairs = false;
   int last = 0;
   for (int d = 0; d <= max_depth; ++d) {
+    if (!known[d] && !pairs_level(d)) {                      // the wave walk needs the count: read it
+      uint32_t cnt = 0;
+      RT_HIP(hipMemcpyAsync(&cnt, A.count + d, 4, hipMemcpyDeviceToHost, st));
+      RT_HIP(hipStreamSynchronize(st));
+      n_level[d] = std::min<uint32_t>(cnt, (uint32_t)cap);
+      known[d] = true;
+    }
+    if (known[d] && n_level[d] == 0) break;
     const uint32_t n = n_level[d];
-    if (n == 0) break;
     last = d;
     A.perm = nullptr;
+    if (pairs_level(d)) {
+      // the pair path reads a level in slot order: its candidate walks are per lane and its evaluations
+      // run in object order (a key sort measured 0.3-0.6 ms per fractal frame slower, profiles/r03o_sort_ab.txt)
+      int rc = wfp_level(c, st, A, std::max(slots, cap), d, known[d] ? n : (uint32_t)cap, known[d] ? nullptr : A.count + d,
+                         a0, a1, a2, a3, max_depth, refr, fc);
+      if (rc) return rc;
+      any_pairs = true;
+      continue;                                              // level d + 1: device-driven
+    }
     if (d > 0) {                                             // this level's slots in key order
       const WfLevel L = wf_level(A, d);                      // host-side pointer arithmetic only
-      // The pair path reads a level in slot order: its candidate walks are per lane and its
-      // evaluations run in object order, and the sort measured 0.3-0.6 ms per fractal frame slower
-      // than none (profiles/r03o_sort_ab.txt).
-      if (!pairs_level(d)) {
 #ifdef RT_WF_RADIX_SORT
-        size_t tb = sort_bytes;
-        RT_HIP(rt_wf_sort_pairs(tmp, &tb, L.key, kout, L.val, perm, (int)n, 30, st));
+      size_t tb = sort_bytes;
+      RT_HIP(rt_wf_sort_pairs(tmp, &tb, L.key, kout, L.val, perm, (int)n, 30, st));
 #else
-        RT_HIP(rt_wf_bucket_sort(L.key, kout, L.val, perm, n, nullptr, RT_WF_LEVEL_BINS, 30 - 12, (uint32_t*)tmp, true, st));
+      RT_HIP(rt_wf_bucket_sort(L.key, kout, L.val, perm, n, nullptr, RT_WF_LEVEL_BINS, 30 - 12, (uint32_t*)tmp, true, st));
 #endif
-        A.perm = perm;
-      }
+      A.perm = perm;
     }
     const dim3 g((n + 63) / 64);
-    if (pairs_level(d)) {
-      uint32_t cnt = 0;
-      int rc = wfp_level(c, st, A, std::max(slots, cap), d, n, a0, a1, a2, a3, max_depth, refr, fc, &cnt);
-      if (rc) return rc;
-      if (d < max_depth) n_level[d + 1] = std::min<uint32_t>(cnt, (uint32_t)cap);
-      continue;
-    }
-    else if (refr && fc) hipLaunchKernelGGL((wf_trace_kernel<true, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
+    if (refr && fc) hipLaunchKernelGGL((wf_trace_kernel<true, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
     else if (refr) hipLaunchKernelGGL((wf_trace_kernel<true, false>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
     else if (fc) hipLaunchKernelGGL((wf_trace_kernel<false, true>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
     else hipLaunchKernelGGL((wf_trace_kernel<false, false>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
     RT_HIP(hipGetLastError());
-    if (d < max_depth) {
-      uint32_t cnt = 0;
-      RT_HIP(hipMemcpyAsync(&cnt, A.count + d + 1, 4, hipMemcpyDeviceToHost, st));
-      RT_HIP(hipStreamSynchronize(st));
-      n_level[d + 1] = std::min<uint32_t>(cnt, (uint32_t)cap);
-    }
   }
   const dim3 bf(256);
   for (int d = last; d >= 0; --d) {
-    const uint32_t n = n_level[d];
-    const dim3 gf((n + 255) / 256);
-    if (f64 && fc) hipLaunchKernelGGL((wf_fold_kernel<true, true>), gf, bf, 0, st, c->dev, A, d, n, a0, a1, a2, a3, target, tstride, rgbi);
-    else if (f64) hipLaunchKernelGGL((wf_fold_kernel<true, false>), gf, bf, 0, st, c->dev, A, d, n, a0, a1, a2, a3, target, tstride, rgbi);
-    else if (fc) hipLaunchKernelGGL((wf_fold_kernel<false, true>), gf, bf, 0, st, c->dev, A, d, n, a0, a1, a2, a3, target, tstride, rgbi);
-    else hipLaunchKernelGGL((wf_fold_kernel<false, false>), gf, bf, 0, st, c->dev, A, d, n, a0, a1, a2, a3, target, tstride, rgbi);
+    const uint32_t n = known[d] ? n_level[d] : (uint32_t)cap;
+    const uint32_t* nd = known[d] ? nullptr : A.count + d;
+    const dim3 gf(std::max(1u, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->n_cu * 8u)));
+    if (f64 && fc) hipLaunchKernelGGL((wf_fold_kernel<true, true>), gf, bf, 0, st, c->dev, A, d, n, nd, a0, a1, a2, a3, target, tstride, rgbi);
+    else if (f64) hipLaunchKernelGGL((wf_fold_kernel<true, false>), gf, bf, 0, st, c->dev, A, d, n, nd, a0, a1, a2, a3, target, tstride, rgbi);
+    else if (fc) hipLaunchKernelGGL((wf_fold_kernel<false, true>), gf, bf, 0, st, c->dev, A, d, n, nd, a0, a1, a2, a3, target, tstride, rgbi);
+    else hipLaunchKernelGGL((wf_fold_kernel<false, false>), gf, bf, 0, st, c->dev, A, d, n, nd, a0, a1, a2, a3, target, tstride, rgbi);
   }
   const dim3 gx((unsigned)c->n_cu * 4u);
 #define RT_WF_FIX(R, F, FCv) hipLaunchKernelGGL((wf_fixup_kernel<R, F, FCv>), gx, dim3(64), 0, st, c->dev, A, a0, a1, a2, a3, max_depth, target, tstride, rgbi)
@@ -973,6 +1005,22 @@ int rt::launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int 
   else { if (fc) RT_WF_FIX(false, false, true); else RT_WF_FIX(false, false, false); }
 #undef RT_WF_FIX
   RT_HIP(hipGetLastError());
+  if (any_pairs) {
+    // the device-driven pair levels' sticky words: ONE host synchronisation per launch (round 4: one per
+    // level).  A level whose pairs outgrew the lists computed wrong hits: grow them to what it needed and
+    // render the launch again (its levels recomputed from the camera rays; the tests force this path)
+    uint32_t ov[2] = {0, 0};
+    RT_HIP(hipMemcpyAsync(ov, A.count + RT_WFP_COUNT + 3, sizeof ov, hipMemcpyDeviceToHost, st));
+    RT_HIP(hipStreamSynchronize(st));
+    if (ov[1]) return fail(RT_ERR_UNSUPPORTED, "wavefront pair count passed 2^31");
+    if (ov[0]) {
+      if (retry > 2) return fail(RT_ERR_DEVICE, "wavefront pair lists still overflow after %d resizes", retry);
+      WfPairs P;
+      int rc = wfp_arena(c, st, std::max(slots, cap), cap, (size_t)ov[0], &P);   // grows (synchronises)
+      if (rc) return rc;
+      return launch_wavefront(c, st, a0, a1, a2, a3, max_depth, target, tstride, f64, rgbi, n_tiles, retry + 1);
+    }
+  }
   return RT_OK;
 }
 

@@ -126,7 +126,7 @@ bool is_device_ptr(const void* p);
 bool diag_env(const char* name);
 // k_wavefront.hip: the wavefront path for rows (y_first, band_rows, band_pitch, n_rows) = a0..a3
 int launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int a3, int max_depth, uint8_t* target,
-                     size_t tstride, bool f64, int rgbi, size_t n_tiles);
+                     size_t tstride, bool f64, int rgbi, size_t n_tiles, int retry = 0);
 // Completion marks (rt_ctx.hip): record one after every launch of the context on stream st; wait for all
 int mark_event(rt_ctx* c, hipStream_t st, hipEvent_t* ev);   // the event a launch on st binds as its stop event
 int mark_launch(rt_ctx* c, hipStream_t st);                  // record it after work enqueued on st (other launches)

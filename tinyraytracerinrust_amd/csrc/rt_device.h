@@ -892,7 +892,7 @@ typedef LDS_AS double lds_f64;
 // Refraction-chain kernels (RT_MODE_CHAIN): frames of the chain stack kept in LDS.  At 4 waves/SIMD
 // (below) 5 frames fill the 160 KB of a CU (10 KB per one-wave workgroup).
 #ifndef RT_LDS_FRAMES_CHAIN
-#define RT_LDS_FRAMES_CHAIN 5
+#define RT_LDS_FRAMES_CHAIN 1
 #endif
 // Refraction frames also carry the pending reflection ray (P, D, rp: 7 doubles); the first
 // KLR of them go to LDS after the KL colour frames, [frame][component][lane] likewise.
@@ -908,9 +908,11 @@ typedef LDS_AS double lds_f64;
 // chains are short leave their share to the long ones: a spinning_globes wave needs ~2 frames per lane
 // on average but up to 10 for some lanes, so the fixed per-lane layout either spilled the deep frames
 // to scratch (KL = 5: 48.7 MB of HBM per 1080p frame) or cost occupancy.  Slots past KP, and frames of
-// pixels whose chain outgrows the pool, use the private array (scratch).  Layout at the wave's base lp:
-// [RT_MAX_DEPTH_CAP] u64 masks, [RT_MAX_DEPTH_CAP] u32 starts, then [4][KP] doubles (component-major:
-// the lanes of one push write consecutive doubles).
+// pixels whose chain outgrows the pool, use the private array (scratch).  The first KL frames of every
+// lane keep their fixed per-lane LDS slots (most chains are that short, and a fixed slot costs no
+// ballot, no rank and no header reads); the pool serves the deeper ones.  Layout at the wave's base lp:
+// [KL][4][64] per-lane frames, [RT_MAX_DEPTH_CAP] u64 masks, [RT_MAX_DEPTH_CAP] u32 starts, then [4][KP]
+// doubles (component-major: the lanes of one push write consecutive doubles).
 constexpr int RT_POOL_HDR = RT_MAX_DEPTH_CAP + RT_MAX_DEPTH_CAP / 2;      // header doubles
 #define LDS_U64 __attribute__((address_space(3))) uint64_t
 #define LDS_U32 __attribute__((address_space(3))) uint32_t
@@ -922,7 +924,8 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {                 // s
 // frame stack.  REFR = the scene has a transparent object (refraction frames need more state).
 // KL > 0: frames 0..KL-1 of the stack are in LDS at lf[(f * 4 + c) * 64] (lf = this lane's slot);
 // KLR > 0 (REFR): the pending-reflection state of frames 0..KLR-1 at lf[(KL * 4 + f * 7 + c) * 64].
-// KP > 0 (not TREE, no recorder): the frames go to the wave's pool of KP slots at lp (above) instead.
+// KP > 0 (not TREE, no recorder): frames KL.. go to the wave's pool of KP slots (above), after the KL
+// per-lane frames at lp.
 // CHAIN (REFR scenes with RtDevScene::ray_chains): every hit spawns at most one ray, so a refraction
 // frame never carries a pending reflection: frames are (A, w) as in the reflection-only kernels.
 template <bool REFR, class Rec = NoRec, int KL = 0, bool FC = false, int KLR = 0, bool CHAIN = false, int KP = 0>
@@ -931,9 +934,10 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
   double fA[RT_MAX_DEPTH_CAP][3];     // parent colour already intensified by (1 - w)
   double fW[RT_MAX_DEPTH_CAP];        // child weight w (transparency or reflectivity)
   constexpr bool POOL = KP > 0 && !(REFR && !CHAIN) && same_type<Rec, NoRec>::value;
-  LDS_U64* const pool_mask = (LDS_U64*)lp;
-  LDS_U32* const pool_start = (LDS_U32*)(lp + RT_MAX_DEPTH_CAP);
-  lds_f64* const pool = lp + RT_POOL_HDR;
+  // frames 0..KL-1 stay in the lanes' own LDS slots (lf); the pool serves frames KL.. (after them at lp)
+  LDS_U64* const pool_mask = (LDS_U64*)(lp + KL * 4 * 64);
+  LDS_U32* const pool_start = (LDS_U32*)(lp + KL * 4 * 64 + RT_MAX_DEPTH_CAP);
+  lds_f64* const pool = lp + KL * 4 * 64 + RT_POOL_HDR;
   uint32_t pool_used = 0;             // wave-uniform: slots taken by the pushes so far
   auto put_frame = [&](int f, Col A, double w) {
     if (KL > 0 && f < KL) {
@@ -943,7 +947,7 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
     }
   };
   auto get_frame = [&](int f, Col* A, double* w) {
-    if constexpr (POOL) {
+    if (POOL && f >= KL) {
       const uint32_t slot = pool_start[f] + lane_rank(pool_mask[f]);
       if (slot < (uint32_t)KP) {
         *A = {pool[slot], pool[KP + slot], pool[2 * KP + slot]}; *w = pool[3 * KP + slot];
@@ -1106,7 +1110,13 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
       }
     }
     if constexpr (RECORD) { if (!descend) rec->finish(slot, C); }     // leaf ray (or miss) reports now
-    if constexpr (POOL) pool_push(pushing, iter, push_A, push_w);        // frame `iter` (= sp before the push)
+    if constexpr (POOL) {                                                // frame `iter` (= sp before the push)
+      if (iter < KL) {
+        if (pushing) put_frame(iter, push_A, push_w);                     // the lane's own LDS slot
+      } else {
+        pool_push(pushing, iter, push_A, push_w);
+      }
+    }
     if (descend) continue;
     while (sp > 0) {                                                      // post-order combine
       const int f = sp - 1;
@@ -1420,15 +1430,28 @@ __device__ __forceinline__ void store_pixel(uint8_t* row, int x, Col c, int rgb)
 // The row kernels' frame storage per one-wave workgroup: the reflection-only and chain modes take a
 // wave pool (trace(), KP slots) by default; KL_ >= 0 asks for KL_ frames per lane instead (the round-4
 // layout, diagnostic A/B); KP_ >= 0 sets the pool's size.  The ray-tree mode keeps per-lane frames.
+// Measured (profiles/r07g_pool_refl_ab.txt, r07h_hybrid_refl_ab.txt; anim120 bench lines r07e-r07h):
+//   reflection-only, 4K globes: 2 per-lane frames 0.3215 ms, 114.7 MB of HBM per launch; a pool of 122
+//     slots 0.3287 ms, 93.1 MB; 2 frames + a pool of 58: 0.3269 ms, 107.9 MB -- chains are short there,
+//     and the pool's ballots and header reads cost more than the scratch they save: no pool;
+//   chain, anim120 (Mrays/s, MB per 1080p frame): 5 per-lane frames (round 4, 10 KB: 4 waves/SIMD)
+//     14 766 / 48.7; 1 per-lane frame 16 251-16 378 / 147.5; 2: 16 149 / 116.5; 1 frame + a pool of 122
+//     (6 KB: 6 waves/SIMD with the family programs' 80 VGPRs) 16 061-16 095 / 93.4; pools of 186 / 250 /
+//     314 slots 16 036 / 15 205 / 14 984 at 92.9 / 67.1 / 46.4 -- 1 frame + 122 is kept: the occupancy of
+//     the fastest layout at 63 % of its traffic.
 #ifndef RT_LDS_POOL_REFL
-#define RT_LDS_POOL_REFL 122        // 4 KB per workgroup, the space of the per-lane KL = 2 frames
+#define RT_LDS_POOL_REFL 0
 #endif
 #ifndef RT_LDS_POOL_CHAIN
-#define RT_LDS_POOL_CHAIN 186       // 6 KB: 26 workgroups per CU, so the VGPRs set the occupancy (5-6 waves/SIMD)
+#define RT_LDS_POOL_CHAIN 122       // + 1 per-lane frame: 6 KB: 26 workgroups per CU, the VGPRs set the occupancy
 #endif
 template <int MODE, int KL_ = -1, int KP_ = -1>
 constexpr int rows_pool_slots() {
-  return KL_ >= 0 || MODE == RT_MODE_TREE ? 0 : KP_ >= 0 ? KP_ : MODE == RT_MODE_CHAIN ? RT_LDS_POOL_CHAIN : RT_LDS_POOL_REFL;
+  return MODE == RT_MODE_TREE ? 0 : KP_ >= 0 ? KP_ : MODE == RT_MODE_CHAIN ? RT_LDS_POOL_CHAIN : RT_LDS_POOL_REFL;
+}
+template <int MODE, int KL_ = -1>
+constexpr int rows_lane_frames() {
+  return KL_ >= 0 ? KL_ : MODE == RT_MODE_CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES;
 }
 template <int MODE, bool F64, bool CAL, bool FC, int KL_ = -1, int KP_ = -1>
 __device__ __forceinline__ void rows_entry(const RtDevScene& S, unsigned entry, int y_first, int band_rows, int band_pitch,
@@ -1438,7 +1461,7 @@ __device__ __forceinline__ void rows_entry(const RtDevScene& S, unsigned entry, 
   constexpr bool REFR = MODE != RT_MODE_REFL, CHAIN = MODE == RT_MODE_CHAIN;
   constexpr int KLR = MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0;
   constexpr int KP = rows_pool_slots<MODE, KL_, KP_>();
-  constexpr int KL = KP > 0 ? 0 : KL_ >= 0 ? KL_ : CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES;
+  constexpr int KL = rows_lane_frames<MODE, KL_>();
   const int lane = threadIdx.x & 63;
   const unsigned tile = CAL || !order ? entry : (unsigned)order[entry];
   [[maybe_unused]] uint64_t t_start = 0;
@@ -1465,10 +1488,8 @@ __device__ __forceinline__ void rows_body(const RtDevScene& S, int y_first, int 
 }
 template <int MODE, int KL_ = -1, int KP_ = -1>
 constexpr int rows_lds_doubles() {
-  return rows_pool_slots<MODE, KL_, KP_>() > 0
-             ? RT_POOL_HDR + 4 * rows_pool_slots<MODE, KL_, KP_>()
-             : ((KL_ >= 0 ? KL_ : MODE == RT_MODE_CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES) * 4 +
-                (MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0) * 7) * 64;
+  return (rows_lane_frames<MODE, KL_>() * 4 + (MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0) * 7) * 64 +
+         (rows_pool_slots<MODE, KL_, KP_>() > 0 ? RT_POOL_HDR + 4 * rows_pool_slots<MODE, KL_, KP_>() : 0);
 }
 
 // The deferred-shadow kernel's body (reflection-only scenes, or refraction chains on request): one
