@@ -23,18 +23,21 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=0)
     ap.add_argument("--generic", action="store_true")
+    ap.add_argument("--levels", default="", help="per library (in order): its RT_OPT_SPECIALIZE level, e.g. 1,2 "
+                                                   "(a library path may repeat); default 1 (0 with --generic)")
     a = ap.parse_args()
     import torch
     scene, W, H, depth = CONFIGS[a.config]
     text = (open(os.path.join(S, scene + ".scene")).read() if scene else "draw(sphere(<0, 0, 0>, 30, red))").encode()
     ctxs, outs = [], []
-    for path in a.libs:
+    levels = [int(v) for v in a.levels.split(",")] if a.levels else [0 if a.generic else 1] * len(a.libs)
+    for path, level in zip(a.libs, levels):
         L = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
         L.rt_ctx_spec_wait.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         sc, cx = ctypes.c_void_p(), ctypes.c_void_p()
         assert L.rt_scene_compile(text, S.encode(), ctypes.c_double(0.0), W, H, ctypes.byref(sc)) == 0
         assert L.rt_ctx_create(0, ctypes.byref(cx)) == 0
-        assert L.rt_ctx_set_option(cx, 6, 0 if a.generic else 1) == 0
+        assert L.rt_ctx_set_option(cx, 6, level) == 0
         assert L.rt_ctx_upload(cx, sc) == 0
         assert L.rt_ctx_spec_wait(cx, -1) == 0
         assert L.rt_ctx_set_option(cx, 1, 0) == 0                  # RT_OPT_TIMING off, as bench.py
@@ -75,9 +78,9 @@ def main():
         if not torch.equal(outs[i], outs[0]):
             raise SystemExit(f"{a.libs[i]}: frame differs from {a.libs[0]}'s")
     print(f"{a.config} ({'generic' if a.generic else 'specialised'}), {n} frames per measurement, ms per frame, median of {a.rounds}:")
-    for path, v in zip(a.libs, res):
+    for path, level, v in zip(a.libs, levels, res):
         w = sorted(v)
-        print(f"  {w[len(w) // 2]:.4f}  ({' '.join(f'{x:.4f}' for x in v)})  {path}", flush=True)
+        print(f"  {w[len(w) // 2]:.4f}  ({' '.join(f'{x:.4f}' for x in v)})  {path} (RT_OPT_SPECIALIZE {level})", flush=True)
 
 
 if __name__ == "__main__":
