@@ -352,7 +352,7 @@ struct WfPairs {
   double* tp;                   // nearest pass: the sorted pair's object's nearest accepted distance
   uint32_t* count;              // [0] / [1]: pairs the nearest / shadow pass emitted (may exceed cap: the host
                                 //   grows the arena and runs the level again); [2]: a count passed 2^31
-  uint32_t* bins;               // bucket-sort scratch (RT_BS_MAX_BINS words)
+  uint32_t* bins;               // bucket-sort scratch: RT_WFP_BIN_WORDS words per sort
   uint32_t cap;
   unsigned long long* tmin;     // per ray of the level: nearest accepted distance (bits; +inf: none)
   int32_t* omin;                // per ray: the least object index at that distance (INT_MAX: none)
@@ -365,6 +365,7 @@ struct WfPairs {
 #endif
 constexpr unsigned long long RT_WFP_NONE = 0x7FF0000000000000ull;   // +inf
 constexpr int RT_WFP_COUNT = 32;      // the pair counts' words in WfArena::count (after the level counts)
+constexpr uint32_t RT_WFP_BIN_WORDS = 4096;   // one bucket sort's scratch (wf_sort.hip: counts + run cursors)
 static_assert(RT_MAX_DEPTH_CAP + 3 <= RT_WFP_COUNT, "wavefront counter block");
 static_assert(RT_WFP_COUNT + 5 <= 64, "wavefront counter block: 256 bytes");
 
@@ -446,9 +447,23 @@ __device__ __forceinline__ bool wf_get_ray(const RtDevScene& S, const WfLevel& l
 // per deep ray on fractal.scene -- the deep levels' dispatches last 45-90 us with a few hundred
 // waves because each wave is that chain (SQ_WAVE_CYCLES counts quad-cycles: the round-3 "8-15 k
 // cycles" per wave are 32-60 k, 15-30 us).  LDS_TRAV: the workgroup (WG_WAVES waves) first copies
-// the hierarchy into LDS and the walks read it there.
+// the hierarchy into LDS and the walks read it there.  Loading the next record beside the box test
+// (the pre-order successor, the next step unless a group misses) measured 9 % slower on the fractal
+// frame (6.02 -> 6.58 ms, profiles/r07q_fractal.txt): kept out.
 constexpr int RT_WFP_CAND_WAVES = 4;
 constexpr uint32_t RT_WFP_LDS_TRAV_MAX = 640;     // nodes (40 KB) staged at most; larger: global loads
+#ifndef RT_WFP_MAX_RANGES_LOG2
+#define RT_WFP_MAX_RANGES_LOG2 2                     // at most 4 hierarchy ranges per ray (below)
+#endif
+#ifndef RT_WFP_HITSORT_MAX_D
+#define RT_WFP_HITSORT_MAX_D 1000                    // levels from this depth on skip the hit-point sort
+#endif
+#ifndef RT_WFP_RANGE_PASSES
+#define RT_WFP_RANGE_PASSES 4                        // ... while the items fill the grid at most 4 times
+#endif
+#ifndef RT_WFP_RANGES_NEAR
+#define RT_WFP_RANGES_NEAR 0                         // 1: the nearest pass's walks too (measured slower)
+#endif
 // n_dev != nullptr (device-driven levels): the level's ray count is min(*n_dev, A.cap), read here; the
 // grid is then a fixed number of workgroups that take the level's rays grid-stride, 64 x WG_WAVES at a
 // time (the hierarchy staged in LDS once per workgroup).
@@ -464,7 +479,20 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
   uint32_t* sk = sk_all[LDS_TRAV ? wv : 0];
   uint32_t* sv = sv_all[LDS_TRAV ? wv : 0];
   if (n_dev) n = min(*n_dev, A.cap);
-  if (blockIdx.x * (64u * WW) >= n) return;                  // no ray for this workgroup: no staging either
+  // Hierarchy ranges: a small level's rays are too few to fill the grid, and its time is the longest
+  // walk of one lane (~100-600 dependent node steps).  There the node array is cut into K equal
+  // contiguous ranges and a lane walks one (ray, range) item: the walk from a range's first node
+  // to its end with the same steps (skip pointers only jump forward; a group that misses covers only
+  // nodes the ray misses too, as its box holds its objects' boxes).  Ancestors outside the range go
+  // untested, so an item may emit pairs the whole walk culls: a superset, which the evaluations
+  // resolve exactly.  K: a power of two, at most 2^RT_WFP_MAX_RANGES_LOG2, n x K within RT_WFP_RANGE_PASSES grids.
+  const uint32_t nthreads = gridDim.x * (64u * WW);
+  uint32_t lk = 0;
+  while (lk < (SHADOW || RT_WFP_RANGES_NEAR ? RT_WFP_MAX_RANGES_LOG2 : 0) &&
+         ((uint64_t)n << (lk + 1)) <= (uint64_t)nthreads * RT_WFP_RANGE_PASSES)
+    ++lk;
+  const uint32_t items = n << lk;
+  if (blockIdx.x * (64u * WW) >= items) return;              // no ray for this workgroup: no staging either
   if constexpr (LDS_TRAV) {                                   // the hierarchy into LDS, once per workgroup
     const uint4* g = (const uint4*)S.trav;
     uint4* l = (uint4*)s_trav;
@@ -509,11 +537,10 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
     }
     nb += c;
   };
-  auto walk = [&](bool act0, V3 o, V3 dir, double tmax, uint32_t id) {
+  auto walk = [&](bool act0, V3 o, V3 dir, double tmax, uint32_t id, int t0, int nt) {   // nodes [t0, nt)
     const CullRay cr = cull_ray(o, dir);
     const RtTrav* __restrict__ TR = LDS_TRAV ? (const RtTrav*)(const void*)s_trav : S.trav;
-    const int nt = S.n_trav;
-    int t = act0 ? 0 : nt;
+    int t = act0 ? t0 : nt;
     while (__ballot(t < nt)) {
       bool h = false;
       int ob = 0;
@@ -531,9 +558,11 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
       emit(h, (uint32_t)ob, id);
     }
   };
-  for (uint32_t base = blockIdx.x * (64u * WW); base < n; base += gridDim.x * (64u * WW)) {   // wave-uniform
-    const uint32_t i = base + threadIdx.x;
-    bool live = i < n;
+  for (uint32_t base = blockIdx.x * (64u * WW); base < items; base += nthreads) {   // wave-uniform
+    const uint32_t q = base + threadIdx.x, i = q >> lk, rg = q & ((1u << lk) - 1u);
+    // this item's range of the node array (the whole array when K = 1)
+    const int t0 = (int)(((uint32_t)S.n_trav * rg) >> lk), t1 = (int)(((uint32_t)S.n_trav * (rg + 1u)) >> lk);
+    bool live = q < items;
     uint32_t j = i;
     V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
     if (live) {
@@ -541,7 +570,7 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
       if (!SHADOW) live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
     }
     if constexpr (!SHADOW) {
-      if (i < n) { P.tmin[j] = RT_WFP_NONE; P.omin[j] = 0x7fffffff; }   // slots outside the frame too
+      if (q < items && rg == 0) { P.tmin[j] = RT_WFP_NONE; P.omin[j] = 0x7fffffff; }   // slots outside the frame too
       // A bound on the nearest hit: the object whose hit spawned the ray, evaluated first (a ray that
       // refracted into or reflects inside a closed shape meets it again).  The walk then tests boxes
       // against [0, cull_tmax(bound)] only -- conservative, as nearest_hit's running best is; the
@@ -558,7 +587,7 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
           if ((mine >> lane) & 1) bound = wfp_object_nearest(D, pu, ro, rd, cr);
         }
       }
-      walk(live, ro, rd, bound < INFINITY ? cull_tmax(bound) : INFINITY, j);
+      walk(live, ro, rd, bound < INFINITY ? cull_tmax(bound) : INFINITY, j, t0, t1);
     } else {
       const int32_t oi = live ? P.omin[j] : 0x7fffffff;
       const bool hit = live && oi != 0x7fffffff;
@@ -575,10 +604,12 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
           len_inv(l, &ll, &ill);
           sdir = scale(l, ill);
           tmax = cull_tmax(ll);
-          P.kcnt[s] = 0;
-          P.opq[s] = 0;
+          if (rg == 0) {
+            P.kcnt[s] = 0;
+            P.opq[s] = 0;
+          }
         }
-        walk(hit, p, sdir, tmax, s);
+        walk(hit, p, sdir, tmax, s, t0, t1);
       }
     }
   }
@@ -733,30 +764,39 @@ __device__ __forceinline__ void wfp_shade_one(RtDevScene S, WfArena A, WfPairs P
 }
 
 
-// End of a device-driven pair level: its pair counts against the arena (a level that emitted more pairs
-// than the lists hold computed wrong nearest hits), kept in sticky words the host reads once per launch:
-// count[RT_WFP_COUNT + 3] = the most pairs any level emitted beyond the capacity, [+ 4] = a count wrapped.
-__global__ void wfp_level_check_kernel(uint32_t* count, uint32_t cap);
+// The pair counter block P.count (RT_WFP_COUNT words into WfArena::count): [0] / [1] the nearest / shadow
+// pairs of the level, [2] a count wrapped; sticky over the launch: [3] the most pairs any level emitted
+// beyond the lists' capacity, [4] any wrap; [5 + 2d] / [6 + 2d] (d <= RT_WFP_LOG_LEVELS) the pairs level
+// d emitted, for diagnostics.
+constexpr int RT_WFP_LOG_LEVELS = (64 - RT_WFP_COUNT - 5) / 2 - 1;
+static_assert(RT_WFP_COUNT + 6 + 2 * RT_WFP_LOG_LEVELS < 64, "wavefront counter block: 256 bytes");
 
 // n_dev != nullptr (device-driven levels): the ray count is min(*n_dev, A.cap); the waves take the
 // level's rays grid-stride, 64 at a time (wf_append: one ballot + one atomic per wave and chunk).
+// The level's last kernel also closes it (every reader of the pair counts and the sort scratch has
+// run): thread 0 checks the pair counts against the lists (a level that emitted more pairs than they
+// hold computed wrong nearest hits: sticky words the host reads once per launch) and zeroes them, and
+// the grid zeroes the three sorts' scratch -- for the next level, with no launches of their own (three
+// per level in round 5's first form: 5 us each on the small levels).
 template <bool REFR, bool FC>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU_WF))) void wfp_shade_kernel(
     RtDevScene S, WfArena A, WfPairs P, int d, uint32_t n, const uint32_t* n_dev, int y_first, int band_rows,
     int band_pitch, int n_rows, int max_depth) {
   const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && lane == 0) {
+    uint32_t* pc = P.count;
+    const uint32_t m = max(pc[0], pc[1]);
+    if (m > P.cap) atomicMax(pc + 3, m);
+    if (pc[2]) atomicOr(pc + 4, 1u);
+    if (d <= RT_WFP_LOG_LEVELS) { pc[5 + 2 * d] = pc[0]; pc[6 + 2 * d] = pc[1]; }
+    pc[0] = pc[1] = pc[2] = 0;
+  }
+  for (uint32_t k = blockIdx.x * 64u + (uint32_t)lane; k < 3u * RT_WFP_BIN_WORDS; k += gridDim.x * 64u) P.bins[k] = 0;
   if (n_dev) n = min(*n_dev, A.cap);
   const WfLevel lv = wf_level(A, d);
   for (uint32_t base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u)   // wave-uniform
     wfp_shade_one<REFR, FC>(S, A, P, lv, d, base + (uint32_t)lane, n, lane, y_first, band_rows, band_pitch, n_rows,
                             max_depth);
-}
-
-__global__ void wfp_level_check_kernel(uint32_t* count, uint32_t cap) {
-  const uint32_t* pc = count + RT_WFP_COUNT;
-  const uint32_t m = max(pc[0], pc[1]);
-  if (m > cap) atomicMax(count + RT_WFP_COUNT + 3, m);
-  if (pc[2]) atomicOr(count + RT_WFP_COUNT + 4, 1u);
 }
 
 }  // namespace
@@ -792,7 +832,7 @@ static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t lcap, size_t ne
     // grows it (RT_OPT_WAVEFRONT_CAP 1 % makes the first size tiny: the overflow tests take that path)
     const size_t cap = std::min<size_t>(0x7fffffc0ull, std::max<size_t>(need + need / 4, 4 * lcap) + 63) & ~(size_t)63;
     if (need > cap) return fail(RT_ERR_UNSUPPORTED, "wavefront pair list of %zu pairs too large", need);
-    const size_t bytes = al(3 * 16384 + 4 * cap * 4 + cap * 8);
+    const size_t bytes = al(3 * RT_WFP_BIN_WORDS * 4 + 4 * cap * 4 + cap * 8);
     if (c->wfp) (void)hipFree(c->wfp);    // waits for launches that may still use it
     c->wfp = nullptr;
     c->wfp_bytes = 0;
@@ -818,7 +858,7 @@ static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t lcap, size_t ne
   P->cap = (uint32_t)cap;
   P->count = nullptr;                   // set by the caller: the wavefront arena's counter block
   P->bins = (uint32_t*)b;               // 3 x RT_BS_MAX_BINS words: nearest / hit-point / shadow sorts
-  P->key = (uint32_t*)(b + 3 * 16384);
+  P->key = (uint32_t*)(b + 3 * RT_WFP_BIN_WORDS * 4);
   P->val = P->key + cap;
   P->key_s = P->val + cap;
   P->val_s = P->key_s + cap;
@@ -835,7 +875,7 @@ static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t lcap, size_t ne
 // lists leaves the sticky overflow word (wfp_level_check_kernel); the host reads it once, after the
 // whole launch, and renders the launch again with lists of that size (launch_wavefront).
 static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int d, uint32_t n_ub, const uint32_t* n_dev,
-                     int a0, int a1, int a2, int a3, int max_depth, bool refr, bool fc) {
+                     int a0, int a1, int a2, int a3, int max_depth, bool refr, bool fc, bool first) {
   WfPairs P;
   int rc = wfp_arena(c, st, R, A.cap, 0, &P);
   if (rc) return rc;
@@ -844,13 +884,20 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
   auto grid = [&](uint32_t per_wg, uint32_t max_wg) { return dim3(std::max(1u, std::min((n_ub + per_wg - 1) / per_wg, max_wg))); };
   const dim3 b64(64);
   const uint32_t nobj = (uint32_t)c->dev.n_objects;
-  uint32_t* bins[3] = {P.bins, P.bins + 4096, P.bins + 8192};
+  uint32_t* bins[3] = {P.bins, P.bins + RT_WFP_BIN_WORDS, P.bins + 2 * RT_WFP_BIN_WORDS};
   // the candidate walks: hierarchies of up to RT_WFP_LDS_TRAV_MAX nodes staged in LDS (4-wave groups)
   const bool lds_trav = (uint32_t)c->dev.n_trav <= RT_WFP_LDS_TRAV_MAX && !diag_env("RT_WFP_GLOBAL_TRAV");
   auto launch_cand = [&](bool shadow) {
     if (lds_trav) {
-      const dim3 gl = grid(64 * RT_WFP_CAND_WAVES, ncu * 16), bl(64 * RT_WFP_CAND_WAVES);
+      // as many workgroups as the CUs hold at once (the LDS-staged hierarchy sets it); they take the
+      // level's rays grid-stride and stage the hierarchy once each (round 5's first form launched
+      // 16 per CU: on the small levels most of them only staged and found no ray)
       const size_t lds = (size_t)c->dev.n_trav * sizeof(RtTrav);
+      int occ = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)(shadow ? wfp_cand_kernel<true, true> : wfp_cand_kernel<false, true>),
+                                                       64 * RT_WFP_CAND_WAVES, lds) != hipSuccess || occ < 1)
+        occ = 1;
+      const dim3 gl = grid(64 * RT_WFP_CAND_WAVES, ncu * (uint32_t)occ), bl(64 * RT_WFP_CAND_WAVES);
       if (shadow) hipLaunchKernelGGL((wfp_cand_kernel<true, true>), gl, bl, lds, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3);
       else hipLaunchKernelGGL((wfp_cand_kernel<false, true>), gl, bl, lds, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3);
     } else if (shadow) {
@@ -864,20 +911,24 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
   // grid-stride evaluations: one pass covers ~4 pairs per ray of the level (fractal: ~3), at most 8
   // waves per SIMD
   const dim3 ge(std::max<uint32_t>(ncu, std::min<uint32_t>((uint32_t)(((size_t)n_ub * 4 + 63) / 64), ncu * 32u)));
-  RT_HIP(hipMemsetAsync(P.count, 0, 12, st));
-  RT_HIP(hipMemsetAsync(P.bins, 0, 3 * 16384, st));        // the three sorts' bucket counters
+  // the pair counters start at zero with the launch's counter block; the sorts' scratch is zeroed here
+  // for the launch's first pair level, by each level's shading kernel for the next
+  if (first) RT_HIP(hipMemsetAsync(P.bins, 0, 3 * RT_WFP_BIN_WORDS * 4, st));
   launch_cand(false);
   RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count, nobj, 0, bins[0], false, st));
   hipLaunchKernelGGL(wfp_near_eval_kernel, ge, b64, 0, st, c->dev, A, P, d, a0, a1, a2, a3);
   hipLaunchKernelGGL(wfp_near_tie_kernel, dim3(std::min<uint32_t>((P.cap + 255) / 256, 4096)), dim3(256), 0, st, P);
-  // the hit points and their order for the shadow and shading passes: at most 4096 buckets of
+  // the hit points and their order for the shadow and shading passes: at most 2048 buckets of
   // (hit object, coarse hit-point cell), unordered within a bucket (a 16^3-cell-only key and the
   // full 27-bit radix sort measured slower: profiles/r03o_sort_ab.txt, r03w_*)
   int cbits = 0;
-  while (cbits < 12 && ((nobj + 1u) << (cbits + 1)) <= 4096u) ++cbits;
+  while (cbits < 12 && ((nobj + 1u) << (cbits + 1)) <= RT_WFP_BIN_WORDS / 2) ++cbits;   // the fused-scan sort's bins
   hipLaunchKernelGGL(wfp_hit_key_kernel, grid(256, ncu * 8), dim3(256), 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3,
                      cbits);
-  RT_HIP(rt_wf_bucket_sort(P.hkey, P.hkey_s, P.hval, P.hperm, n_ub, n_dev, (nobj + 1u) << cbits, 0, bins[1], false, st));
+  if (d < RT_WFP_HITSORT_MAX_D)
+    RT_HIP(rt_wf_bucket_sort(P.hkey, P.hkey_s, P.hval, P.hperm, n_ub, n_dev, (nobj + 1u) << cbits, 0, bins[1], false, st));
+  else
+    P.hperm = P.hval;                     // the level's own order (hval[i] = the i-th ray's slot)
   launch_cand(true);
   RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count + 1, nobj, 0, bins[2], false, st));
   hipLaunchKernelGGL(wfp_shadow_eval_kernel, ge, b64, 0, st, c->dev, P);
@@ -886,7 +937,6 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
   else if (refr) hipLaunchKernelGGL((wfp_shade_kernel<true, false>), gs, b64, 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3, max_depth);
   else if (fc) hipLaunchKernelGGL((wfp_shade_kernel<false, true>), gs, b64, 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3, max_depth);
   else hipLaunchKernelGGL((wfp_shade_kernel<false, false>), gs, b64, 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3, max_depth);
-  hipLaunchKernelGGL(wfp_level_check_kernel, dim3(1), dim3(1), 0, st, A.count, P.cap);
   RT_HIP(hipGetLastError());
   return RT_OK;
 }
@@ -965,7 +1015,7 @@ int rt::launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int 
       // the pair path reads a level in slot order: its candidate walks are per lane and its evaluations
       // run in object order (a key sort measured 0.3-0.6 ms per fractal frame slower, profiles/r03o_sort_ab.txt)
       int rc = wfp_level(c, st, A, std::max(slots, cap), d, known[d] ? n : (uint32_t)cap, known[d] ? nullptr : A.count + d,
-                         a0, a1, a2, a3, max_depth, refr, fc);
+                         a0, a1, a2, a3, max_depth, refr, fc, !any_pairs);
       if (rc) return rc;
       any_pairs = true;
       continue;                                              // level d + 1: device-driven
@@ -1012,6 +1062,16 @@ int rt::launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int 
     uint32_t ov[2] = {0, 0};
     RT_HIP(hipMemcpyAsync(ov, A.count + RT_WFP_COUNT + 3, sizeof ov, hipMemcpyDeviceToHost, st));
     RT_HIP(hipStreamSynchronize(st));
+    static const bool wf_debug = diag_env("RT_WF_DEBUG");
+    if (wf_debug) {                       // per level: rays, nearest pairs, shadow pairs
+      uint32_t cb[64];
+      RT_HIP(hipMemcpy(cb, A.count, sizeof cb, hipMemcpyDeviceToHost));
+      fprintf(stderr, "wavefront levels (rays / nearest pairs / shadow pairs):");
+      for (int d = 0; d <= last && d <= RT_WFP_LOG_LEVELS; ++d)
+        fprintf(stderr, " %d: %u / %u / %u;", d, d == 0 ? (uint32_t)slots : cb[d], cb[RT_WFP_COUNT + 5 + 2 * d],
+                cb[RT_WFP_COUNT + 6 + 2 * d]);
+      fprintf(stderr, "\n");
+    }
     if (ov[1]) return fail(RT_ERR_UNSUPPORTED, "wavefront pair count passed 2^31");
     if (ov[0]) {
       if (retry > 2) return fail(RT_ERR_DEVICE, "wavefront pair lists still overflow after %d resizes", retry);

@@ -31,7 +31,13 @@ extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const u
 //            the L2s of the 8 XCDs -- measured 3.6x slower hist, profiles/r05z_wavefront_round4.txt);
 //   scatter: per workgroup a contiguous chunk: LDS counts give each item its rank among the chunk's
 //            items of its key, one atomic per nonzero bin reserves the chunk's run in that bucket.
+// Sorts of at most RT_BS_FUSED_BINS bins (the pair lists: one bin per object; the hit points) skip the
+// scan launch: every scatter workgroup scans the counts itself in LDS (2 K words at most) and reserves
+// its runs on a second, zeroed word per bin (cnt[RT_BS_FUSED_BINS + b]): a launch boundary costs
+// 4-6 us on the pair path's small levels (profiles/r07k_fractal_kernel_stats.csv), the scan of 2 K
+// words a fraction of one.
 #define RT_BS_MAX_BINS 4096
+#define RT_BS_FUSED_BINS 2048
 #define RT_BS_THREADS 256
 #define RT_BS_PER_THREAD 16
 __device__ __forceinline__ uint32_t rt_bs_bin(uint32_t key, int shift, uint32_t nb) {
@@ -78,10 +84,38 @@ __global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_scatter(const uint32_t* _
                                                               const uint32_t* __restrict__ n_dev, uint32_t nb,
                                                               int shift, uint32_t* __restrict__ off,
                                                               uint32_t* __restrict__ keys_out,
-                                                              uint32_t* __restrict__ vals_out) {
+                                                              uint32_t* __restrict__ vals_out, int fused) {
   if (n_dev) n = min(*n_dev, n);
   __shared__ uint32_t h[RT_BS_MAX_BINS];
+  __shared__ uint32_t pre[RT_BS_FUSED_BINS];                 // fused: the exclusive offsets of the bins
   constexpr uint32_t CH = RT_BS_THREADS * RT_BS_PER_THREAD;
+  if (blockIdx.x * CH >= n) return;
+  if (fused) {                                               // off[] holds the counts: scan them here
+    constexpr uint32_t PER = RT_BS_FUSED_BINS / RT_BS_THREADS;
+    const uint32_t b0 = threadIdx.x * PER;
+    uint32_t v[PER], s = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < PER; ++e) {
+      v[e] = b0 + e < nb ? off[b0 + e] : 0u;
+      s += v[e];
+    }
+    h[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < RT_BS_THREADS; o <<= 1) {        // inclusive scan of the thread sums
+      const uint32_t a = threadIdx.x >= o ? h[threadIdx.x - o] : 0u;
+      __syncthreads();
+      h[threadIdx.x] += a;
+      __syncthreads();
+    }
+    uint32_t run = h[threadIdx.x] - s;
+#pragma unroll
+    for (uint32_t e = 0; e < PER; ++e) {
+      pre[b0 + e] = run;
+      run += v[e];
+    }
+    __syncthreads();
+  }
+  uint32_t* const cur = off + RT_BS_FUSED_BINS;
   for (uint32_t base = blockIdx.x * CH; base < n; base += gridDim.x * CH) {   // chunks, grid-stride
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
     __syncthreads();
@@ -94,7 +128,7 @@ __global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_scatter(const uint32_t* _
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
-      if (h[b]) h[b] = atomicAdd(&off[b], h[b]);            // this chunk's run in bucket b
+      if (h[b]) h[b] = fused ? pre[b] + atomicAdd(&cur[b], h[b]) : atomicAdd(&off[b], h[b]);   // this chunk's run in bucket b
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < RT_BS_PER_THREAD; ++e) {
@@ -110,23 +144,25 @@ __global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_scatter(const uint32_t* _
 }
 
 // Sorts n (key, value) pairs by bin = min(key >> shift, nb - 1) (nb <= RT_BS_MAX_BINS) into keys_out
-// (the bins) / vals_out; cnt: nb words of device scratch.  n_dev != nullptr: the count is
+// (the bins) / vals_out; cnt: device scratch of nb words, or 2 x RT_BS_FUSED_BINS words when nb <=
+// RT_BS_FUSED_BINS (the fused scan's counts and run cursors).  n_dev != nullptr: the count is
 // min(*n_dev, n), read on the device (n is then the capacity the grids are sized for).  zero_cnt =
-// false: the caller already zeroed cnt[0, nb) on this stream.
+// false: the caller already zeroed that scratch on this stream.
 extern "C" hipError_t rt_wf_bucket_sort(const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
                                         uint32_t* vals_out, uint32_t n, const uint32_t* n_dev, uint32_t nb, int shift,
                                         uint32_t* cnt, bool zero_cnt, hipStream_t stream) {
   if (nb == 0 || nb > RT_BS_MAX_BINS) return hipErrorInvalidValue;
   if (n == 0) return hipSuccess;
+  const int fused = nb <= RT_BS_FUSED_BINS ? 1 : 0;
   if (zero_cnt) {
-    hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nb * 4, stream);
+    hipError_t e = hipMemsetAsync(cnt, 0, (size_t)(fused ? 2 * RT_BS_FUSED_BINS : nb) * 4, stream);
     if (e != hipSuccess) return e;
   }
   const uint32_t chunk = RT_BS_THREADS * RT_BS_PER_THREAD, gc = (n + chunk - 1) / chunk;
   hipLaunchKernelGGL(rt_bs_hist, dim3(std::min<uint32_t>(gc, 1024u)), dim3(RT_BS_THREADS), 0, stream, keys_in, n, n_dev,
                      nb, shift, cnt);
-  hipLaunchKernelGGL(rt_bs_scan, dim3(1), dim3(1024), 0, stream, cnt, nb);
+  if (!fused) hipLaunchKernelGGL(rt_bs_scan, dim3(1), dim3(1024), 0, stream, cnt, nb);
   hipLaunchKernelGGL(rt_bs_scatter, dim3(std::min<uint32_t>(gc, 2048u)), dim3(RT_BS_THREADS), 0, stream, keys_in,
-                     vals_in, n, n_dev, nb, shift, cnt, keys_out, vals_out);
+                     vals_in, n, n_dev, nb, shift, cnt, keys_out, vals_out, fused);
   return hipGetLastError();
 }
