@@ -24,8 +24,8 @@ namespace {
 //                    the next pass then traces rays that start close together in similar directions,
 //                    so the wave-coherent traversal walks fewer objects (the megakernel's waves walk the
 //                    union of what their lanes' scattered secondary rays need);
-//   wf_fold_kernel   after every level is traced, from the deepest level up: a ray's colour from its
-//                    hit record and its children's colours (already folded into their L slots):
+//   wf_fold_kernel   after every level is traced, from the deepest level up (RT_WF_FOLD_SPAN levels
+//                    per launch): a ray's colour from its hit record and its children's colours:
 //                      refraction child: comb = in_range(L.intensify(1 - t) + C_t.intensify(t)),
 //                      then a reflection child: in_range(comb.intensify(1 - rp) + C_r.intensify(rp)),
 //                    exactly the post-order of raytracer.rs:256-279 (trace()'s frame fold).  Level 0's
@@ -222,6 +222,10 @@ __device__ __forceinline__ void wf_append(const WfArena& A, const WfLevel& lv, i
   }
 }
 
+#ifndef RT_WF_FOLD_SPAN
+#define RT_WF_FOLD_SPAN 3                // levels folded per launch (1..3)
+#endif
+static_assert(RT_WF_FOLD_SPAN >= 1 && RT_WF_FOLD_SPAN <= 3, "fold span");
 #ifndef RT_WAVES_PER_EU_WF
 #define RT_WAVES_PER_EU_WF 5
 #endif
@@ -256,27 +260,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER
   wf_append(A, lv, d, lane, live, j, pix, L, wt, wr, ch_t, ch_r, p, dt, dr, oi);
 }
 
-template <bool F64, bool FC>
+// The folded colour of ray i of level d: its hit record and its children's colours -- computed here
+// for the SPAN - 1 levels below d (a child has one parent: nothing is computed twice), read as stored
+// (already folded) at level d + SPAN.  The same operations in the same order as one fold per level.
+template <int SPAN, bool FC>
+__device__ __forceinline__ Col wf_fold_node(const WfArena& A, int d, uint32_t i) {
+  const WfLevel lv = wf_level(A, d);
+  const Col L = {lv.Lr[i], lv.Lg[i], lv.Lb[i]};
+  const int32_t ct = lv.ct[i], cr = lv.cr[i];
+  auto child = [&](int32_t c) -> Col {
+    if constexpr (SPAN > 1) {
+      return wf_fold_node<SPAN - 1, FC>(A, d + 1, (uint32_t)c);
+    } else {
+      const WfLevel ch = wf_level(A, d + 1);
+      return Col{ch.Lr[c], ch.Lg[c], ch.Lb[c]};
+    }
+  };
+  Col C = L;
+  if (ct >= 0) {                                             // refraction, then a pending reflection
+    const double t = lv.wt[i];
+    C = cadd<FC>(intensify<FC>(L, 1.0 - t), intensify<FC>(child(ct), t));
+  }
+  if (cr >= 0) {
+    const double w = lv.wr[i];
+    C = cadd<FC>(intensify<FC>(C, 1.0 - w), intensify<FC>(child(cr), w));
+  }
+  return C;
+}
+
+// Folds SPAN levels per launch (d .. d + SPAN - 1; level d's colours stored, or level 0's written as
+// pixels): one launch boundary per SPAN levels (a boundary costs ~5 us on the pair path's small levels).
+template <int SPAN, bool F64, bool FC>
 __global__ __launch_bounds__(256) void wf_fold_kernel(RtDevScene S, WfArena A, int d, uint32_t n, const uint32_t* n_dev,
                                                       int y_first, int band_rows, int band_pitch, int n_rows,
                                                       uint8_t* __restrict__ out, size_t stride, int rgb) {
   if (n_dev) n = min(*n_dev, A.cap);                         // a device-driven level's count
   const WfLevel lv = wf_level(A, d);
-  const WfLevel ch = wf_level(A, d + 1);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int x = 0, r = 0, y = 0;
     if (d == 0 && (!wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y) || A.ovf[i])) continue;
-    const Col L = {lv.Lr[i], lv.Lg[i], lv.Lb[i]};
-    const int32_t ct = lv.ct[i], cr = lv.cr[i];
-    Col C = L;
-    if (ct >= 0) {                                             // refraction, then a pending reflection
-      const double t = lv.wt[i];
-      C = cadd<FC>(intensify<FC>(L, 1.0 - t), intensify<FC>(Col{ch.Lr[ct], ch.Lg[ct], ch.Lb[ct]}, t));
-    }
-    if (cr >= 0) {
-      const double w = lv.wr[i];
-      C = cadd<FC>(intensify<FC>(C, 1.0 - w), intensify<FC>(Col{ch.Lr[cr], ch.Lg[cr], ch.Lb[cr]}, w));
-    }
+    const Col C = wf_fold_node<SPAN, FC>(A, d, i);
     if (d > 0) {
       lv.Lr[i] = C.r; lv.Lg[i] = C.g; lv.Lb[i] = C.b;
       continue;
@@ -461,8 +484,8 @@ constexpr uint32_t RT_WFP_LDS_TRAV_MAX = 640;     // nodes (40 KB) staged at mos
 #ifndef RT_WFP_RANGE_PASSES
 #define RT_WFP_RANGE_PASSES 4                        // ... while the items fill the grid at most 4 times
 #endif
-#ifndef RT_WFP_RANGES_NEAR
-#define RT_WFP_RANGES_NEAR 0                         // 1: the nearest pass's walks too (measured slower)
+#ifndef RT_WFP_NEAR_RANGES_LOG2
+#define RT_WFP_NEAR_RANGES_LOG2 1                    // the nearest pass's walks: at most 2 ranges (8 measured slower)
 #endif
 // n_dev != nullptr (device-driven levels): the level's ray count is min(*n_dev, A.cap), read here; the
 // grid is then a fixed number of workgroups that take the level's rays grid-stride, 64 x WG_WAVES at a
@@ -488,7 +511,7 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
   // resolve exactly.  K: a power of two, at most 2^RT_WFP_MAX_RANGES_LOG2, n x K within RT_WFP_RANGE_PASSES grids.
   const uint32_t nthreads = gridDim.x * (64u * WW);
   uint32_t lk = 0;
-  while (lk < (SHADOW || RT_WFP_RANGES_NEAR ? RT_WFP_MAX_RANGES_LOG2 : 0) &&
+  while (lk < (SHADOW ? RT_WFP_MAX_RANGES_LOG2 : RT_WFP_NEAR_RANGES_LOG2) &&
          ((uint64_t)n << (lk + 1)) <= (uint64_t)nthreads * RT_WFP_RANGE_PASSES)
     ++lk;
   const uint32_t items = n << lk;
@@ -1037,15 +1060,24 @@ int rt::launch_wavefront(rt_ctx* c, hipStream_t st, int a0, int a1, int a2, int 
     else hipLaunchKernelGGL((wf_trace_kernel<false, false>), g, dim3(64), 0, st, c->dev, A, d, n, a0, a1, a2, a3, max_depth);
     RT_HIP(hipGetLastError());
   }
+  // the folds, deepest level first, RT_WF_FOLD_SPAN levels per launch; the deepest level's rays have no
+  // children (their colour is their hit record) unless it is level 0, which writes the pixels
   const dim3 bf(256);
-  for (int d = last; d >= 0; --d) {
+  for (int top = last > 0 ? last - 1 : 0; top >= 0;) {
+    const int d = std::max(0, top - RT_WF_FOLD_SPAN + 1), span = top - d + 1;
     const uint32_t n = known[d] ? n_level[d] : (uint32_t)cap;
     const uint32_t* nd = known[d] ? nullptr : A.count + d;
     const dim3 gf(std::max(1u, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->n_cu * 8u)));
-    if (f64 && fc) hipLaunchKernelGGL((wf_fold_kernel<true, true>), gf, bf, 0, st, c->dev, A, d, n, nd, a0, a1, a2, a3, target, tstride, rgbi);
-    else if (f64) hipLaunchKernelGGL((wf_fold_kernel<true, false>), gf, bf, 0, st, c->dev, A, d, n, nd, a0, a1, a2, a3, target, tstride, rgbi);
-    else if (fc) hipLaunchKernelGGL((wf_fold_kernel<false, true>), gf, bf, 0, st, c->dev, A, d, n, nd, a0, a1, a2, a3, target, tstride, rgbi);
-    else hipLaunchKernelGGL((wf_fold_kernel<false, false>), gf, bf, 0, st, c->dev, A, d, n, nd, a0, a1, a2, a3, target, tstride, rgbi);
+#define RT_WF_FOLD(SP)                                                                                                  \
+  if (f64 && fc) hipLaunchKernelGGL((wf_fold_kernel<SP, true, true>), gf, bf, 0, st, c->dev, A, d, n, nd, a0, a1, a2, a3, target, tstride, rgbi); \
+  else if (f64) hipLaunchKernelGGL((wf_fold_kernel<SP, true, false>), gf, bf, 0, st, c->dev, A, d, n, nd, a0, a1, a2, a3, target, tstride, rgbi); \
+  else if (fc) hipLaunchKernelGGL((wf_fold_kernel<SP, false, true>), gf, bf, 0, st, c->dev, A, d, n, nd, a0, a1, a2, a3, target, tstride, rgbi); \
+  else hipLaunchKernelGGL((wf_fold_kernel<SP, false, false>), gf, bf, 0, st, c->dev, A, d, n, nd, a0, a1, a2, a3, target, tstride, rgbi);
+    if (span >= 3) { RT_WF_FOLD(3) }
+    else if (span == 2) { RT_WF_FOLD(2) }
+    else { RT_WF_FOLD(1) }
+#undef RT_WF_FOLD
+    top = d - 1;
   }
   const dim3 gx((unsigned)c->n_cu * 4u);
 #define RT_WF_FIX(R, F, FCv) hipLaunchKernelGGL((wf_fixup_kernel<R, F, FCv>), gx, dim3(64), 0, st, c->dev, A, a0, a1, a2, a3, max_depth, target, tstride, rgbi)

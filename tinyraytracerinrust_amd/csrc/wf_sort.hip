@@ -48,11 +48,27 @@ __global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_hist(const uint32_t* __re
                                                            const uint32_t* __restrict__ n_dev, uint32_t nb, int shift,
                                                            uint32_t* __restrict__ cnt) {
   if (n_dev) n = min(*n_dev, n);
+  // contiguous chunks of RT_BS_THREADS x RT_BS_PER_THREAD items, as the scatter takes them: a workgroup
+  // past the count leaves at once, and every thread issues its chunk's loads before its LDS atomics.
+  // (Round 5's first form strode the whole grid over the items: on the pair path's device-driven levels
+  // the grid is sized for the lists' capacity, and 1024 workgroups each added ~all bins to cnt[] --
+  // 13-20 us of same-address atomics for a 100-640 k item level, profiles/r07r_fractal_levels_trace.txt.)
+  constexpr uint32_t CH = RT_BS_THREADS * RT_BS_PER_THREAD;
+  if (blockIdx.x * CH >= n) return;
   __shared__ uint32_t h[RT_BS_MAX_BINS];
   for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
   __syncthreads();
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    atomicAdd(&h[rt_bs_bin(keys[i], shift, nb)], 1u);
+  for (uint32_t base = blockIdx.x * CH; base < n; base += gridDim.x * CH) {
+    uint32_t k[RT_BS_PER_THREAD];
+#pragma unroll
+    for (int e = 0; e < RT_BS_PER_THREAD; ++e) {
+      const uint32_t i = base + (uint32_t)e * RT_BS_THREADS + threadIdx.x;
+      k[e] = i < n ? keys[i] : 0xffffffffu;
+    }
+#pragma unroll
+    for (int e = 0; e < RT_BS_PER_THREAD; ++e)
+      if (base + (uint32_t)e * RT_BS_THREADS + threadIdx.x < n) atomicAdd(&h[rt_bs_bin(k[e], shift, nb)], 1u);
+  }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
     if (h[b]) atomicAdd(&cnt[b], h[b]);
