@@ -79,7 +79,7 @@ __device__ __forceinline__ bool wf_pixel(const RtDevScene& S, uint32_t slot, int
                                          int n_rows, int* x, int* r, int* y) {
   tile_pixel(slot >> 6, (int)(slot & 63), S.width, x, r);
   if (*x >= S.width || *r >= n_rows) return false;
-  *y = y_first + (*r / band_rows) * band_pitch + *r % band_rows;
+  *y = band_row(*r, y_first, band_rows, band_pitch, n_rows);
   return *y < S.height;
 }
 // coherence key of a ray: direction octant (3 bits) above the 27-bit Morton code of its origin's
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER
   if (d == 0) {
     int x, r, y;
     live = live && wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y);
-    if (live) camera_ray(S.cam, (double)x, (double)y, &ro, &rd);          // get_pixel(x as f64, y as f64)
+    if (live) camera_ray_px(S, x, y, &ro, &rd);                          // get_pixel(x as f64, y as f64)
   } else if (live) {
     j = A.perm ? A.perm[i] : i;
     ro = {lv.ox[j], lv.oy[j], lv.oz[j]};
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(64) void wf_fixup_kernel(RtDevScene S, WfArena A, i
     int x, r, y;
     if (!A.ovf[i] || !wf_pixel(S, i, y_first, band_rows, band_pitch, n_rows, &x, &r, &y)) continue;
     V3 ro, rd;
-    camera_ray(S.cam, (double)x, (double)y, &ro, &rd);
+    camera_ray_px(S, x, y, &ro, &rd);
     const Col C = trace<REFR, NoRec, 0, FC>(make_ds(S), ro, rd, max_depth);
     uint8_t* row = out + (size_t)r * stride;
     if constexpr (F64) {
@@ -452,7 +452,7 @@ __device__ __forceinline__ bool wf_get_ray(const RtDevScene& S, const WfLevel& l
   if (d == 0) {
     int x, r, y;
     if (!wf_pixel(S, j, y_first, band_rows, band_pitch, n_rows, &x, &r, &y)) return false;
-    camera_ray(S.cam, (double)x, (double)y, ro, rd);
+    camera_ray_px(S, x, y, ro, rd);
     return true;
   }
   *ro = {lv.ox[j], lv.oy[j], lv.oz[j]};

@@ -206,4 +206,8 @@ struct RtDevScene {
                                     // one value, shadow_t (scene.cpp flatten; the wavefront pair path)
   double shadow_t;
   RtCamera cam;
+  // get_pixel(x as f64, y as f64)'s per-column and per-row camera terms for integer pixels (rt_ctx
+  // upload, the host's IEEE evaluation of camera_ray's own expressions): width and height doubles
+  const double* cam_sx;
+  const double* cam_sy;
 };

@@ -141,6 +141,13 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
          o_leaves = put(blob, f.leaves);
   size_t o_prog = put(blob, f.prog), o_lights = put(blob, f.lights), o_tex = put(blob, f.textures);
   size_t o_texels = put(blob, f.texels);
+  // camera_ray's terms of the integer pixels (rt_device.h camera_ray_px): the same expressions in the
+  // same order, IEEE double on the host (-ffp-contract=off as the device), so a table entry is the
+  // value the device would compute
+  std::vector<double> csx((size_t)std::max(0, f.width)), csy((size_t)std::max(0, f.height));
+  for (size_t x = 0; x < csx.size(); ++x) csx[x] = (((double)x / f.cam.width) - 0.5) * f.cam.aspect;
+  for (size_t y = 0; y < csy.size(); ++y) csy[y] = (f.cam.height - 1.0 - (double)y) / f.cam.height - 0.5;
+  size_t o_csx = put(blob, csx), o_csy = put(blob, csy);
   RT_HIP(hipSetDevice(c->device));
   RT_TRY(rt::wait_launches(c));       // launches in flight read the blob and may run the specialised modules
   if (c->d_blob) { (void)hipFree(c->d_blob); c->d_blob = nullptr; }
@@ -161,6 +168,8 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   d.lights = (const RtLight*)(b + o_lights);
   d.textures = (const RtTexture*)(b + o_tex);
   d.texels = b + o_texels;
+  d.cam_sx = (const double*)(b + o_csx);
+  d.cam_sy = (const double*)(b + o_csy);
   d.n_objects = (int32_t)f.objects.size();
   d.n_lights = (int32_t)f.lights.size();
   d.n_leaves = (int32_t)f.leaves.size();

@@ -1345,6 +1345,15 @@ __device__ __forceinline__ void camera_ray(const RtCamera& cam, double x, double
   *ro = ld3(cam.center);
 }
 
+// The same ray for an integer pixel (x, y) in the frame: the two divisions and their terms read from
+// the upload's per-column / per-row tables (RtDevScene::cam_sx / cam_sy, computed by the host with
+// camera_ray's expressions), the rest as camera_ray.
+__device__ __forceinline__ void camera_ray_px(const RtDevScene& S, int x, int y, V3* ro, V3* rd) {
+  const double sx = S.cam_sx[x], sy = S.cam_sy[y];
+  *rd = add(add(ld3(S.cam.direction), scale(ld3(S.cam.right), sx)), scale(ld3(S.cam.up), sy));
+  *ro = ld3(S.cam.center);
+}
+
 // Output rows r = 0 .. n_rows-1 of a band layout: r -> full-frame row
 //   y = y_first + (r / band_rows) * band_pitch + r % band_rows
 // (a contiguous tile [y0, y1) is one band; the cyclic multi-GPU layout deals bands of
@@ -1384,6 +1393,13 @@ __device__ __forceinline__ void tile_pixel(unsigned tile, int pix, int width, in
   const unsigned tiles_x = (unsigned)(width + RT_TILE_W - 1) / RT_TILE_W;
   *x = (int)(tile % tiles_x) * RT_TILE_W + pix % RT_TILE_W;
   *r = (int)(tile / tiles_x) * RT_TILE_H + pix / RT_TILE_W;
+}
+
+// Output row r of a launch -> its frame row (see above); a launch of one band (every single-GPU frame)
+// skips the per-lane integer division and remainder (a wave-uniform branch).
+__device__ __forceinline__ int band_row(int r, int y_first, int band_rows, int band_pitch, int n_rows) {
+  if (band_rows >= n_rows) return y_first + r;
+  return y_first + (r / band_rows) * band_pitch + r % band_rows;
 }
 
 // One pixel's colour into an output row: f64 RGBA (alpha 1 after any colour op), packed RGB8 (band
@@ -1469,10 +1485,10 @@ __device__ __forceinline__ void rows_entry(const RtDevScene& S, unsigned entry, 
   int x, r;
   tile_pixel(tile, lane, S.width, &x, &r);
   if (x >= S.width || r >= n_rows) return;
-  const int y = y_first + (r / band_rows) * band_pitch + r % band_rows;
+  const int y = band_row(r, y_first, band_rows, band_pitch, n_rows);
   if (y >= S.height) return;
   V3 ro, rd;
-  camera_ray(S.cam, (double)x, (double)y, &ro, &rd);                       // get_pixel(x as f64, y as f64)
+  camera_ray_px(S, x, y, &ro, &rd);                                         // get_pixel(x as f64, y as f64)
   const Col c = trace<REFR, NoRec, KL, FC, KLR, CHAIN, KP>(make_ds(S), ro, rd, max_depth, nullptr, frames + lane, frames);
   store_pixel<F64>(out + (size_t)r * stride, x, c, rgb);
   if constexpr (CAL)
@@ -1514,11 +1530,11 @@ __device__ __forceinline__ void deferred_body(const RtDevScene& S, int y_first, 
   int y = 0;
   bool valid = lane < per && x < S.width && r < n_rows;
   if (valid) {
-    y = y_first + (r / band_rows) * band_pitch + r % band_rows;
+    y = band_row(r, y_first, band_rows, band_pitch, n_rows);
     valid = y < S.height;
   }
   V3 ro = {0.0, 0.0, 0.0}, rd = {0.0, 0.0, 0.0};
-  if (valid) camera_ray(S.cam, (double)x, (double)y, &ro, &rd);             // get_pixel(x as f64, y as f64)
+  if (valid) camera_ray_px(S, x, y, &ro, &rd);                              // get_pixel(x as f64, y as f64)
   const Col c = trace_deferred<RT_MAX_DEPTH_CAP + 1, FC, REFR>(make_ds(S), ro, rd, max_depth, valid, win);
   if (valid) store_pixel<F64>(out + (size_t)r * stride, x, c, rgb);
   if constexpr (CAL)
