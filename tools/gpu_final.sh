@@ -18,9 +18,10 @@ if [ "${TESTS:-1}" = "1" ]; then
   tail -2 $O/${T}_pytest_gpu.txt
 fi
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/${T}_bench.json 2> $O/${T}_bench.err || { tail $O/${T}_bench.err; exit 1; }
+# the config lines at bench.py's own defaults (50 steps, 10 warmup; anim120 3 animations of 120 frames)
 for C in sphere1080d0 globes1080d5 anim120; do
-  S=20; [ $C = anim120 ] && S=3
-  timeout -k 10 400 python bench.py --config $C --steps $S --warmup 2 > $O/${T}_bench_$C.json 2> $O/${T}_bench_$C.err || { tail $O/${T}_bench_$C.err; exit 1; }
+  F=""; [ $C = anim120 ] && F="--steps 3 --warmup 2"
+  timeout -k 10 400 python bench.py --config $C $F > $O/${T}_bench_$C.json 2> $O/${T}_bench_$C.err || { tail $O/${T}_bench_$C.err; exit 1; }
 done
 for PMC in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64" "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES" "SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT"; do
   N=$(echo $PMC | tr ' ' '_' | cut -c1-40)
