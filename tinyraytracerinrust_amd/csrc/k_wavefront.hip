@@ -478,6 +478,9 @@ constexpr uint32_t RT_WFP_LDS_TRAV_MAX = 640;     // nodes (40 KB) staged at mos
 #ifndef RT_WFP_MAX_RANGES_LOG2
 #define RT_WFP_MAX_RANGES_LOG2 2                     // at most 4 hierarchy ranges per ray (below)
 #endif
+#ifndef RT_WFP_CAND_COUNTS
+#define RT_WFP_CAND_COUNTS 1                         // the candidate kernels count their pairs for the sorts
+#endif
 #ifndef RT_WFP_HITSORT_MAX_D
 #define RT_WFP_HITSORT_MAX_D 1000                    // levels from this depth on skip the hit-point sort
 #endif
@@ -494,10 +497,13 @@ template <bool SHADOW, bool LDS_TRAV>
 __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevScene S, WfArena A, WfPairs P, int d,
                                                                           uint32_t n, const uint32_t* n_dev,
                                                                           int y_first, int band_rows, int band_pitch,
-                                                                          int n_rows) {
+                                                                          int n_rows, uint32_t* __restrict__ hcnt) {
   constexpr int WW = LDS_TRAV ? RT_WFP_CAND_WAVES : 1;
   __shared__ uint32_t sk_all[WW][RT_WFP_BUF], sv_all[WW][RT_WFP_BUF];
   extern __shared__ __attribute__((aligned(16))) uint8_t s_trav[];
+  // hcnt != nullptr: the pairs' histogram by object for the bucket sort (its histogram launch skipped),
+  // counted in LDS (after the staged hierarchy) and added to hcnt once per workgroup
+  uint32_t* const s_hist = (uint32_t*)(s_trav + (LDS_TRAV ? (size_t)S.n_trav * sizeof(RtTrav) : 0));
   const int lane = threadIdx.x & 63, wv = (int)(threadIdx.x >> 6);
   uint32_t* sk = sk_all[LDS_TRAV ? wv : 0];
   uint32_t* sv = sv_all[LDS_TRAV ? wv : 0];
@@ -516,12 +522,14 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
     ++lk;
   const uint32_t items = n << lk;
   if (blockIdx.x * (64u * WW) >= items) return;              // no ray for this workgroup: no staging either
+  if (hcnt)
+    for (uint32_t b = threadIdx.x; b < (uint32_t)S.n_objects; b += blockDim.x) s_hist[b] = 0;
   if constexpr (LDS_TRAV) {                                   // the hierarchy into LDS, once per workgroup
     const uint4* g = (const uint4*)S.trav;
     uint4* l = (uint4*)s_trav;
     for (uint32_t q = threadIdx.x; q < (uint32_t)S.n_trav * (sizeof(RtTrav) / 16); q += blockDim.x) l[q] = g[q];
-    __syncthreads();
   }
+  if (LDS_TRAV || hcnt) __syncthreads();
   const WfLevel lv = wf_level(A, d);
   const DS D = make_ds(S);
   uint32_t nb = 0;                                           // wave-uniform fill of the LDS buffer
@@ -543,8 +551,14 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
       if (base >= 0x80000000u) atomicOr(P.count + 2, 1u);
     }
     base = (uint32_t)__shfl((int)base, 0);
+    // the histogram counts the pairs the list holds (a level that overflows it is rendered again, but
+    // its sort must still see counts that match the stored keys: no unwritten slot is read)
     for (uint32_t q = (uint32_t)lane; q < nb; q += 64)
-      if (base + q < P.cap) { P.key[base + q] = sk[q]; P.val[base + q] = sv[q]; }
+      if (base + q < P.cap) {
+        P.key[base + q] = sk[q];
+        P.val[base + q] = sv[q];
+        if (hcnt) atomicAdd(&s_hist[sk[q]], 1u);
+      }
     wave_sync();
     nb = 0;
   };
@@ -637,6 +651,11 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
     }
   }
   flush();
+  if (hcnt) {                                                // every wave of the workgroup is done
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < (uint32_t)S.n_objects; b += blockDim.x)
+      if (s_hist[b]) atomicAdd(&hcnt[b], s_hist[b]);
+  }
 }
 
 // One lane per sorted pair: the waves see one object (two at a run boundary): scalarised over the
@@ -828,7 +847,7 @@ using namespace rt;
 
 extern "C" hipError_t rt_wf_bucket_sort(const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
                                         uint32_t* vals_out, uint32_t n, const uint32_t* n_dev, uint32_t nb, int shift,
-                                        uint32_t* cnt, bool zero_cnt, hipStream_t stream);
+                                        uint32_t* cnt, bool zero_cnt, hipStream_t stream, bool counted = false);
 #ifdef RT_WF_RADIX_SORT
 extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                                        const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit,
@@ -910,25 +929,29 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
   uint32_t* bins[3] = {P.bins, P.bins + RT_WFP_BIN_WORDS, P.bins + 2 * RT_WFP_BIN_WORDS};
   // the candidate walks: hierarchies of up to RT_WFP_LDS_TRAV_MAX nodes staged in LDS (4-wave groups)
   const bool lds_trav = (uint32_t)c->dev.n_trav <= RT_WFP_LDS_TRAV_MAX && !diag_env("RT_WFP_GLOBAL_TRAV");
+  // the candidate kernels count their pairs by object for the sorts (fused-scan sorts: <= 2048 objects)
+  const bool counted = nobj <= RT_WFP_BIN_WORDS / 2 && RT_WFP_CAND_COUNTS;
+  const size_t hist_lds = counted ? (size_t)nobj * 4 : 0;
   auto launch_cand = [&](bool shadow) {
+    uint32_t* hc = counted ? bins[shadow ? 2 : 0] : nullptr;
     if (lds_trav) {
       // as many workgroups as the CUs hold at once (the LDS-staged hierarchy sets it); they take the
       // level's rays grid-stride and stage the hierarchy once each (round 5's first form launched
       // 16 per CU: on the small levels most of them only staged and found no ray)
-      const size_t lds = (size_t)c->dev.n_trav * sizeof(RtTrav);
+      const size_t lds = (size_t)c->dev.n_trav * sizeof(RtTrav) + hist_lds;
       int occ = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)(shadow ? wfp_cand_kernel<true, true> : wfp_cand_kernel<false, true>),
                                                        64 * RT_WFP_CAND_WAVES, lds) != hipSuccess || occ < 1)
         occ = 1;
       const dim3 gl = grid(64 * RT_WFP_CAND_WAVES, ncu * (uint32_t)occ), bl(64 * RT_WFP_CAND_WAVES);
-      if (shadow) hipLaunchKernelGGL((wfp_cand_kernel<true, true>), gl, bl, lds, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3);
-      else hipLaunchKernelGGL((wfp_cand_kernel<false, true>), gl, bl, lds, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3);
+      if (shadow) hipLaunchKernelGGL((wfp_cand_kernel<true, true>), gl, bl, lds, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3, hc);
+      else hipLaunchKernelGGL((wfp_cand_kernel<false, true>), gl, bl, lds, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3, hc);
     } else if (shadow) {
-      hipLaunchKernelGGL((wfp_cand_kernel<true, false>), grid(64, ncu * 64), b64, 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1,
-                         a2, a3);
+      hipLaunchKernelGGL((wfp_cand_kernel<true, false>), grid(64, ncu * 64), b64, hist_lds, st, c->dev, A, P, d, n_ub, n_dev,
+                         a0, a1, a2, a3, hc);
     } else {
-      hipLaunchKernelGGL((wfp_cand_kernel<false, false>), grid(64, ncu * 64), b64, 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1,
-                         a2, a3);
+      hipLaunchKernelGGL((wfp_cand_kernel<false, false>), grid(64, ncu * 64), b64, hist_lds, st, c->dev, A, P, d, n_ub, n_dev,
+                         a0, a1, a2, a3, hc);
     }
   };
   // grid-stride evaluations: one pass covers ~4 pairs per ray of the level (fractal: ~3), at most 8
@@ -938,7 +961,7 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
   // for the launch's first pair level, by each level's shading kernel for the next
   if (first) RT_HIP(hipMemsetAsync(P.bins, 0, 3 * RT_WFP_BIN_WORDS * 4, st));
   launch_cand(false);
-  RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count, nobj, 0, bins[0], false, st));
+  RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count, nobj, 0, bins[0], false, st, counted));
   hipLaunchKernelGGL(wfp_near_eval_kernel, ge, b64, 0, st, c->dev, A, P, d, a0, a1, a2, a3);
   hipLaunchKernelGGL(wfp_near_tie_kernel, dim3(std::min<uint32_t>((P.cap + 255) / 256, 4096)), dim3(256), 0, st, P);
   // the hit points and their order for the shadow and shading passes: at most 2048 buckets of
@@ -946,6 +969,8 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
   // full 27-bit radix sort measured slower: profiles/r03o_sort_ab.txt, r03w_*)
   int cbits = 0;
   while (cbits < 12 && ((nobj + 1u) << (cbits + 1)) <= RT_WFP_BIN_WORDS / 2) ++cbits;   // the fused-scan sort's bins
+  // (the hit-key kernel counting its keys for this sort, over contiguous 4096-ray chunks, measured
+  // slower: 5.63 vs 5.50 ms, profiles/r08a_fractal.txt)
   hipLaunchKernelGGL(wfp_hit_key_kernel, grid(256, ncu * 8), dim3(256), 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3,
                      cbits);
   if (d < RT_WFP_HITSORT_MAX_D)
@@ -953,7 +978,7 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
   else
     P.hperm = P.hval;                     // the level's own order (hval[i] = the i-th ray's slot)
   launch_cand(true);
-  RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count + 1, nobj, 0, bins[2], false, st));
+  RT_HIP(rt_wf_bucket_sort(P.key, P.key_s, P.val, P.val_s, P.cap, P.count + 1, nobj, 0, bins[2], false, st, counted));
   hipLaunchKernelGGL(wfp_shadow_eval_kernel, ge, b64, 0, st, c->dev, P);
   const dim3 gs = grid(64, ncu * 32);
   if (refr && fc) hipLaunchKernelGGL((wfp_shade_kernel<true, true>), gs, b64, 0, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3, max_depth);

@@ -101,19 +101,34 @@ __global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_scatter(const uint32_t* _
                                                               int shift, uint32_t* __restrict__ off,
                                                               uint32_t* __restrict__ keys_out,
                                                               uint32_t* __restrict__ vals_out, int fused) {
+  const uint32_t cap = n;                                    // the output lists' capacity
   if (n_dev) n = min(*n_dev, n);
   __shared__ uint32_t h[RT_BS_MAX_BINS];
   __shared__ uint32_t pre[RT_BS_FUSED_BINS];                 // fused: the exclusive offsets of the bins
   constexpr uint32_t CH = RT_BS_THREADS * RT_BS_PER_THREAD;
   if (blockIdx.x * CH >= n) return;
+  // a chunk's keys and values are loaded before the work that does not need them (the first chunk's
+  // during the fused scan, the next chunk's after this one's stores are issued): the small levels'
+  // scatters are latency chains
+  uint32_t k[RT_BS_PER_THREAD], v[RT_BS_PER_THREAD], r[RT_BS_PER_THREAD];
+  auto load = [&](uint32_t base) {
+#pragma unroll
+    for (int e = 0; e < RT_BS_PER_THREAD; ++e) {
+      const uint32_t i = base + (uint32_t)e * RT_BS_THREADS + threadIdx.x;
+      k[e] = i < n ? rt_bs_bin(keys[i], shift, nb) : 0u;
+      v[e] = i < n ? vals[i] : 0u;
+    }
+  };
+  uint32_t base = blockIdx.x * CH;
+  load(base);
   if (fused) {                                               // off[] holds the counts: scan them here
     constexpr uint32_t PER = RT_BS_FUSED_BINS / RT_BS_THREADS;
     const uint32_t b0 = threadIdx.x * PER;
-    uint32_t v[PER], s = 0;
+    uint32_t c[PER], s = 0;
 #pragma unroll
     for (uint32_t e = 0; e < PER; ++e) {
-      v[e] = b0 + e < nb ? off[b0 + e] : 0u;
-      s += v[e];
+      c[e] = b0 + e < nb ? off[b0 + e] : 0u;
+      s += c[e];
     }
     h[threadIdx.x] = s;
     __syncthreads();
@@ -127,19 +142,17 @@ __global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_scatter(const uint32_t* _
 #pragma unroll
     for (uint32_t e = 0; e < PER; ++e) {
       pre[b0 + e] = run;
-      run += v[e];
+      run += c[e];
     }
     __syncthreads();
   }
   uint32_t* const cur = off + RT_BS_FUSED_BINS;
-  for (uint32_t base = blockIdx.x * CH; base < n; base += gridDim.x * CH) {   // chunks, grid-stride
+  while (true) {                                             // chunks, grid-stride
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
     __syncthreads();
-    uint32_t k[RT_BS_PER_THREAD], r[RT_BS_PER_THREAD];
 #pragma unroll
     for (int e = 0; e < RT_BS_PER_THREAD; ++e) {
       const uint32_t i = base + (uint32_t)e * RT_BS_THREADS + threadIdx.x;
-      k[e] = i < n ? rt_bs_bin(keys[i], shift, nb) : 0u;
       r[e] = i < n ? atomicAdd(&h[k[e]], 1u) : 0u;
     }
     __syncthreads();
@@ -150,12 +163,18 @@ __global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_scatter(const uint32_t* _
     for (int e = 0; e < RT_BS_PER_THREAD; ++e) {
       const uint32_t i = base + (uint32_t)e * RT_BS_THREADS + threadIdx.x;
       if (i < n) {
+        // (q < cap: the counts are those of the stored items; the bound guards the lists regardless)
         const uint32_t q = h[k[e]] + r[e];
-        keys_out[q] = k[e];
-        vals_out[q] = vals[i];
+        if (q < cap) {
+          keys_out[q] = k[e];
+          vals_out[q] = v[e];
+        }
       }
     }
+    base += gridDim.x * CH;
+    if (base >= n) break;
     __syncthreads();
+    load(base);
   }
 }
 
@@ -163,20 +182,23 @@ __global__ __launch_bounds__(RT_BS_THREADS) void rt_bs_scatter(const uint32_t* _
 // (the bins) / vals_out; cnt: device scratch of nb words, or 2 x RT_BS_FUSED_BINS words when nb <=
 // RT_BS_FUSED_BINS (the fused scan's counts and run cursors).  n_dev != nullptr: the count is
 // min(*n_dev, n), read on the device (n is then the capacity the grids are sized for).  zero_cnt =
-// false: the caller already zeroed that scratch on this stream.
+// false: the caller already zeroed that scratch on this stream.  counted: the kernel that wrote the
+// keys also added their bins' counts into cnt[0, nb) (no histogram launch; the fused scan only).
 extern "C" hipError_t rt_wf_bucket_sort(const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
                                         uint32_t* vals_out, uint32_t n, const uint32_t* n_dev, uint32_t nb, int shift,
-                                        uint32_t* cnt, bool zero_cnt, hipStream_t stream) {
+                                        uint32_t* cnt, bool zero_cnt, hipStream_t stream, bool counted) {
   if (nb == 0 || nb > RT_BS_MAX_BINS) return hipErrorInvalidValue;
   if (n == 0) return hipSuccess;
   const int fused = nb <= RT_BS_FUSED_BINS ? 1 : 0;
+  if (counted && (!fused || zero_cnt)) return hipErrorInvalidValue;
   if (zero_cnt) {
     hipError_t e = hipMemsetAsync(cnt, 0, (size_t)(fused ? 2 * RT_BS_FUSED_BINS : nb) * 4, stream);
     if (e != hipSuccess) return e;
   }
   const uint32_t chunk = RT_BS_THREADS * RT_BS_PER_THREAD, gc = (n + chunk - 1) / chunk;
-  hipLaunchKernelGGL(rt_bs_hist, dim3(std::min<uint32_t>(gc, 1024u)), dim3(RT_BS_THREADS), 0, stream, keys_in, n, n_dev,
-                     nb, shift, cnt);
+  if (!counted)
+    hipLaunchKernelGGL(rt_bs_hist, dim3(std::min<uint32_t>(gc, 1024u)), dim3(RT_BS_THREADS), 0, stream, keys_in, n, n_dev,
+                       nb, shift, cnt);
   if (!fused) hipLaunchKernelGGL(rt_bs_scan, dim3(1), dim3(1024), 0, stream, cnt, nb);
   hipLaunchKernelGGL(rt_bs_scatter, dim3(std::min<uint32_t>(gc, 2048u)), dim3(RT_BS_THREADS), 0, stream, keys_in,
                      vals_in, n, n_dev, nb, shift, cnt, keys_out, vals_out, fused);
