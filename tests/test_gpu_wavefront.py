@@ -179,3 +179,29 @@ def test_wavefront_pairs_small_scenes(text, d, pairs):
     gu, gf = _render(text, 0.0, W, H, d, pairs=pairs)
     rf, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H, f64=True)
     assert_close(gu, gf, ru, rf, f"wavefront pairs={pairs} small scene d={d}")
+
+
+def _sphere_field(n, seed):
+    """n small spheres spread over the default camera's view, glass spheres that also reflect among
+    them (ray trees), and a reflective floor: a hierarchy of ~2n nodes."""
+    import random
+    r = random.Random(seed)
+    lines = ["draw(plane(<0, 1, 0>, 32, white * 0.6, 0.3))"]
+    mats = ["red, 0.3, 0.6", "blue, 0, 0.6", "white * 0.8, 0.5, 0", "rgb(0.2, 0.9, 0.4), 0, 0"]   # one transparency: shadow_pow
+    for k in range(n):
+        c = f"<{r.uniform(-40, 40):.2f}, {r.uniform(-28, 28):.2f}, {r.uniform(-25, 45):.2f}>"
+        lines.append(f"draw(sphere({c}, {r.uniform(0.8, 3.5):.2f}, {mats[k % len(mats)]}))")
+    return "\n".join(lines)
+
+
+@pytest.mark.parametrize("n", [400, 2100])
+def test_wavefront_pairs_large_hierarchies(n):
+    """Scenes past the candidate walks' LDS hierarchy (> 640 nodes: the walks read the node array from
+    global memory) and, at 2100 objects, past the fused-scan sorts (> 2048 buckets: the candidate
+    kernels count no pairs, the sorts launch their histogram and scan): every pixel against the oracle."""
+    from oracle import oracle as O
+    text = _sphere_field(n, 7000 + n)
+    W, H, d = 96, 72, 6
+    gu, gf = _render(text, 0.0, W, H, d, pairs=2)
+    rf, ru = O.OracleScene(text, 0.0, W, H, max_depth=d).render(0, H, f64=True)
+    assert_close(gu, gf, ru, rf, f"wavefront pairs, {n} objects")
