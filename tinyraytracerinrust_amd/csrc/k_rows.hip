@@ -66,49 +66,6 @@ using namespace rt;
 #define RT_ORDER_MIN_TILES 2048
 #endif
 
-// The RGBA8 frame's 128-byte lines each hold one row of `group` horizontally adjacent 8x8 tiles.
-// Cost-sorted, those tiles run at different times on different XCDs (workgroups are dealt to the 8
-// XCDs round-robin: entries e and e + 8 share one), and every tile's row segment leaves its XCD's L2
-// as a partial-line write.  The XCD-aware order keeps the cost sort at the granularity of a line's
-// tiles (their costliest first) and places one line's tiles at entries e, e + 8, e + 16, ... of a
-// block of 8 x group entries: one XCD renders them back to back and its L2 merges their stores.
-// Measured (profiles/r07n_xcd_order_ab.txt, a diagnostic build with RT_ORDER_XCD=1): the stores do NOT
-// merge -- WRITE_SIZE per 4K globes launch 78.0 -> 114.2 MiB, per anim120 frame 49.5 -> 57.0 MiB --
-// and the time is mixed: 4K 0.3229 -> 0.3223 ms, 1080p d5 0.0892 -> 0.0881, the sphere 0.0191 ->
-// 0.0185, anim120 16 099 / 16 032 -> 15 841 / 15 817 Mrays/s.  Off.
-#ifndef RT_ORDER_XCD
-#define RT_ORDER_XCD 0
-#endif
-static void xcd_line_order(std::vector<int32_t>& order, const std::vector<uint32_t>& cost, int tiles_x, int group,
-                           bool interleave) {
-  const size_t n = order.size(), nq = n / (size_t)group, qx = (size_t)(tiles_x / group);
-  std::vector<uint32_t> qcost(nq, 0);
-  for (size_t t = 0; t < n; ++t) {
-    const size_t q = (t / (size_t)tiles_x) * qx + (t % (size_t)tiles_x) / (size_t)group;
-    qcost[q] = std::max(qcost[q], cost[t]);
-  }
-  std::vector<int32_t> qorder(nq);
-  for (size_t q = 0; q < nq; ++q) qorder[q] = (int32_t)q;
-  std::stable_sort(qorder.begin(), qorder.end(), [&](int32_t x, int32_t y) { return qcost[x] > qcost[y]; });
-  size_t e = 0;
-  if (!interleave) {                      // diagnostic (RT_ORDER_XCD=2): the line's tiles at consecutive entries
-    for (size_t k = 0; k < nq; ++k)
-      for (int j = 0; j < group; ++j) {
-        const size_t q = (size_t)qorder[k];
-        order[e++] = (int32_t)((q / qx) * (size_t)tiles_x + (q % qx) * (size_t)group + (size_t)j);
-      }
-    return;
-  }
-  for (size_t g = 0; g < nq; g += 8) {
-    const size_t m = std::min<size_t>(8, nq - g);
-    for (int j = 0; j < group; ++j)
-      for (size_t i = 0; i < m; ++i) {
-        const size_t q = (size_t)qorder[g + i];
-        order[e++] = (int32_t)((q / qx) * (size_t)tiles_x + (q % qx) * (size_t)group + (size_t)j);
-      }
-  }
-}
-
 static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_t band_pitch, uint32_t n_bands,
                         int32_t max_depth, void* out, size_t stride, void* stream, bool f64, bool rgb = false) {
   if (!c || !out) return fail(RT_ERR_INVALID, "null argument");
@@ -323,10 +280,6 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
       tail_bound = (double)mx > (double)sum / slots;
     }
     slot->deferred = eligible && (dmode == 1 || tail_bound);
-    const int line_tiles = 128 / (RT_TILE_W * 4);
-    if (RT_ORDER_XCD && !slot->deferred && !f64 && !rgbi && tiles_x % line_tiles == 0 && tstride % 128 == 0 &&
-        ((uintptr_t)target & 127) == 0)
-      xcd_line_order(h_order, h_cost, tiles_x, line_tiles, RT_ORDER_XCD == 1);
     if (slot->deferred) {
       // Split the costliest tiles over P = 2, 4 or 8 waves (cost >= k * P * the median tile):
       // their shadow rays then spread over P x 64 lanes.  The factor k: 1 below 24000 tiles, 1.5
