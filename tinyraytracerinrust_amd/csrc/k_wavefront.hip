@@ -914,7 +914,7 @@ static int wfp_arena(rt_ctx* c, hipStream_t st, size_t R, size_t lcap, size_t ne
 // level 0) or min(A.count[d], cap), read by the kernels themselves (n_dev); the pair counts stay on the
 // device too (the sorts and the evaluations read them).  Grids are fixed and the kernels take their
 // work grid-stride, so the host launches every level back to back.  A level whose pairs outgrew the
-// lists leaves the sticky overflow word (wfp_level_check_kernel); the host reads it once, after the
+// lists leaves the sticky overflow word (checked by the level's shading kernel); the host reads it once, after the
 // whole launch, and renders the launch again with lists of that size (launch_wavefront).
 static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int d, uint32_t n_ub, const uint32_t* n_dev,
                      int a0, int a1, int a2, int a3, int max_depth, bool refr, bool fc, bool first) {

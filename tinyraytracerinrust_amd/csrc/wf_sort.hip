@@ -21,7 +21,7 @@ extern "C" hipError_t rt_wf_sort_pairs(void* d_temp, size_t* temp_bytes, const u
 
 // ---------------------------------------------------------------------------- bucket sort
 // The pair path's sort of (object, pair) by object: few keys (the scene's objects), many items.  A
-// counting sort in three launches (a radix sort of a few million items takes a dozen: rocPRIM's
+// counting sort in three launches at most (a radix sort of a few million items takes a dozen: rocPRIM's
 // block sort + merge passes below its one-sweep size), not stable -- the pair order within an
 // object does not matter (k_wavefront.hip wfp_*: the folds are atomic min / add / or).
 //   hist:    per workgroup an LDS histogram of its grid-stride share, added to cnt[] (one atomic per
