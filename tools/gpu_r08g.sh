@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round 5: sign-uniform box tests (RT_BOX_SIGNS) against the previous library: the GPU suite first,
+# then interleaved A/B on the BASELINE configs and the fractal frame.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out
+mkdir -p $O
+T=${TAG:-r08g}
+P=tinyraytracerinrust_amd/librt_mi355x.so
+V=tinyraytracerinrust_amd/build/librt_mi355x_prev.so
+( while sleep 50; do date +%T >> $O/${T}_heartbeat.txt; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
+timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/${T}_pytest_gpu.txt 2>&1 || { tail -40 $O/${T}_pytest_gpu.txt; exit 1; }
+tail -2 $O/${T}_pytest_gpu.txt
+for C in globes4k sphere1080d0 globes1080d5; do
+  timeout -k 10 300 python -u tools/ab_libs.py $V $P --config $C >> $O/${T}_ab.txt 2>&1 || { tail -20 $O/${T}_ab.txt; exit 1; }
+done
+grep -v amdgpu.ids $O/${T}_ab.txt
+for L in $V $P; do
+  RT_LIB_PATH=$L timeout -k 10 300 python -u tools/scene_timing.py fractal 1920x1080 0 10 wavefront:p1 7 2>&1 | grep -v amdgpu.ids | sed "s|\$| [$(basename $L)]|" >> $O/${T}_fractal.txt || exit 1
+done
+cat $O/${T}_fractal.txt
+echo session done
