@@ -939,10 +939,13 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
       // level's rays grid-stride and stage the hierarchy once each (round 5's first form launched
       // 16 per CU: on the small levels most of them only staged and found no ray)
       const size_t lds = (size_t)c->dev.n_trav * sizeof(RtTrav) + hist_lds;
-      int occ = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)(shadow ? wfp_cand_kernel<true, true> : wfp_cand_kernel<false, true>),
-                                                       64 * RT_WFP_CAND_WAVES, lds) != hipSuccess || occ < 1)
-        occ = 1;
+      int& occ = c->wfp_occ[shadow ? 1 : 0];                    // queried once per context and LDS size
+      if (occ < 1 || c->wfp_occ_lds[shadow ? 1 : 0] != lds) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)(shadow ? wfp_cand_kernel<true, true> : wfp_cand_kernel<false, true>),
+                                                         64 * RT_WFP_CAND_WAVES, lds) != hipSuccess || occ < 1)
+          occ = 1;
+        c->wfp_occ_lds[shadow ? 1 : 0] = lds;
+      }
       const dim3 gl = grid(64 * RT_WFP_CAND_WAVES, ncu * (uint32_t)occ), bl(64 * RT_WFP_CAND_WAVES);
       if (shadow) hipLaunchKernelGGL((wfp_cand_kernel<true, true>), gl, bl, lds, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3, hc);
       else hipLaunchKernelGGL((wfp_cand_kernel<false, true>), gl, bl, lds, st, c->dev, A, P, d, n_ub, n_dev, a0, a1, a2, a3, hc);

@@ -37,6 +37,8 @@ struct rt_ctx {
   void* wf = nullptr;                   // wavefront arena (levels, counters, overflow flags), grow-only
   size_t wf_bytes = 0;
   int wf_pairs = 1;                     // rt_ctx_set_option(RT_OPT_WAVEFRONT_PAIRS): 0 off, 1 levels >= 1, 2 every level
+  int wfp_occ[2] = {0, 0};              // candidate kernels (nearest, shadow): workgroups per CU at wfp_occ_lds bytes of LDS
+  size_t wfp_occ_lds[2] = {0, 0};
   void* wfr = nullptr;                  // pair path: per-ray arrays (nearest hit, hit point, shadow counts), grow-only
   size_t wfr_bytes = 0;
   void* wfp = nullptr;                  // pair path: pair lists + sort scratch, grow-only
