@@ -284,7 +284,13 @@ static std::string spec_kernel(int kind, int mode, bool fc, int f64, int cal) {
 #ifndef RT_SPEC_WAVES
 #define RT_SPEC_WAVES 4
 #endif
-  snprintf(waves, sizeof waves, "%d", RT_SPEC_WAVES);
+// Chain-mode programs (the anim120 families: 82 VGPRs, 6 waves/SIMD set by the VGPRs and the 6 KB of
+// LDS frames) at 7 waves (72 VGPRs, 11 spilled, a 100-110-slot pool) measured 0.5-1 % slower
+// (profiles/r08j_chain_waves_ab.txt).  Diagnostic builds may set RT_SPEC_WAVES_CHAIN.
+#ifndef RT_SPEC_WAVES_CHAIN
+#define RT_SPEC_WAVES_CHAIN RT_SPEC_WAVES
+#endif
+  snprintf(waves, sizeof waves, "%d", mode == RT_MODE_CHAIN ? RT_SPEC_WAVES_CHAIN : RT_SPEC_WAVES);
   // stack frames in LDS: 4 waves/SIMD leave 10 KB per one-wave workgroup (the generic kernel's 2
   // frames at 5 waves: 4 KB); RT_SPEC_LDS_FRAMES (diagnostic builds) overrides the mode's default
 #ifdef RT_SPEC_LDS_FRAMES
