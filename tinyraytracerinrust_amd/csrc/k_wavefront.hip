@@ -485,7 +485,7 @@ constexpr uint32_t RT_WFP_LDS_TRAV_MAX = 640;     // nodes (40 KB) staged at mos
 #define RT_WFP_HITSORT_MAX_D 1000                    // levels from this depth on skip the hit-point sort
 #endif
 #ifndef RT_WFP_RANGE_PASSES
-#define RT_WFP_RANGE_PASSES 4                        // ... while the items fill the grid at most 4 times
+#define RT_WFP_RANGE_PASSES 8                        // ... while the items fill the grid at most 8 times (4: +0.8 %)
 #endif
 #ifndef RT_WFP_NEAR_RANGES_LOG2
 #define RT_WFP_NEAR_RANGES_LOG2 1                    // the nearest pass's walks: at most 2 ranges (8 measured slower)
