@@ -473,7 +473,10 @@ __device__ __forceinline__ bool wf_get_ray(const RtDevScene& S, const WfLevel& l
 // the hierarchy into LDS and the walks read it there.  Loading the next record beside the box test
 // (the pre-order successor, the next step unless a group misses) measured 9 % slower on the fractal
 // frame (6.02 -> 6.58 ms, profiles/r07q_fractal.txt): kept out.
-constexpr int RT_WFP_CAND_WAVES = 4;
+#ifndef RT_WFP_CAND_WAVES_N
+#define RT_WFP_CAND_WAVES_N 4
+#endif
+constexpr int RT_WFP_CAND_WAVES = RT_WFP_CAND_WAVES_N;
 constexpr uint32_t RT_WFP_LDS_TRAV_MAX = 640;     // nodes (40 KB) staged at most; larger: global loads
 #ifndef RT_WFP_MAX_RANGES_LOG2
 #define RT_WFP_MAX_RANGES_LOG2 2                     // at most 4 hierarchy ranges per ray (below)
