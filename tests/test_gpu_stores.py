@@ -94,3 +94,27 @@ def test_split_tiles_4k_share(worldmap):
         torch.cuda.synchronize()
         got = slot.cpu().numpy()[:ref.shape[0]]
         assert np.array_equal(got, ref), f"launch {launch}: {int((got != ref).sum())} channels differ ({r.kernel_info()})"
+
+
+@pytest.mark.parametrize("W,pad,depth", [(512, 0, 0), (512, 128, 0), (512, 4, 0), (520, 0, 0), (512, 0, 10)])
+def test_cached_frame_stores_and_xcd_order(worldmap, W, pad, depth):
+    """Primary-ray (max_depth 0) RGBA8 frames of at most RT_CACHED_FRAME_BYTES (k_rows.hip) take plain
+    stores through the L2s and, when their rows are whole 128-byte lines (tiles_x % 4 == 0, 128-byte
+    pitch and base), the XCD-aware tile order on ordered launches; other pitches and widths keep the
+    cost order, deeper launches streaming stores.  >= 2048 tiles, so the calibration launch and two
+    ordered launches each give the oracle's bits, padding untouched."""
+    import torch
+    H = 256
+    text = scene_text("globes")
+    r = _rt(text, W, H, depth=depth)
+    pitch = W * 4 + pad
+    ref = _ref(text, W, H, depth=depth)
+    buf = torch.full((pitch * H + 256,), 0xA5, dtype=torch.uint8, device="cuda")
+    for launch in ("calibration", "ordered", "ordered again"):
+        r.render_rows_into(0, H, buf.data_ptr(), pitch)
+        torch.cuda.synchronize()
+        host = buf.cpu().numpy()
+        rows = np.stack([host[y * pitch: y * pitch + W * 4] for y in range(H)]).reshape(H, W, 4)
+        assert np.array_equal(rows, ref), f"{W} pad {pad} {launch}: {int((rows != ref).sum())} channels differ"
+        gaps = [host[y * pitch + W * 4: (y + 1) * pitch] for y in range(H - 1)]
+        assert all((g == 0xA5).all() for g in gaps)
