@@ -66,6 +66,38 @@ using namespace rt;
 #define RT_ORDER_MIN_TILES 2048
 #endif
 
+// Primary-ray launches (max_depth 0: one intersection and its shading per pixel, so the frame's
+// stores are a large share of the kernel) take an XCD-aware tile order.  The RGBA8 frame's 128-byte
+// lines each hold one row of `group` horizontally adjacent 8x8 tiles; cost-sorted, those tiles run at
+// different times on different XCDs (workgroups are dealt to the 8 XCDs round-robin: entries e and
+// e + 8 share one).  The XCD-aware order keeps the cost sort at the granularity of a line's tiles
+// (their costliest first) and places one line's tiles at entries e, e + 8, e + 16, ... of a block of
+// 8 x group entries: one XCD renders them back to back.  Measured on every launch
+// (profiles/r07n_xcd_order_ab.txt): the sphere 1080p d0 -3 %, globes 1080p d5 -1.2 %, 4K -0.2 %, but
+// anim120 1.6 % slower and the partial-line writes do not merge (4K WRITE_SIZE +36 MiB); with plain
+// stores as well the sphere gains 9 % but a store-policy branch costs the deeper launches up to 3 %
+// (profiles/r08o_xcdp_ab.txt, r08q_cached_ab.txt) -- so the order alone, for max_depth 0 only.
+static void xcd_line_order(std::vector<int32_t>& order, const std::vector<uint32_t>& cost, int tiles_x, int group) {
+  const size_t n = order.size(), nq = n / (size_t)group, qx = (size_t)(tiles_x / group);
+  std::vector<uint32_t> qcost(nq, 0);
+  for (size_t t = 0; t < n; ++t) {
+    const size_t q = (t / (size_t)tiles_x) * qx + (t % (size_t)tiles_x) / (size_t)group;
+    qcost[q] = std::max(qcost[q], cost[t]);
+  }
+  std::vector<int32_t> qorder(nq);
+  for (size_t q = 0; q < nq; ++q) qorder[q] = (int32_t)q;
+  std::stable_sort(qorder.begin(), qorder.end(), [&](int32_t x, int32_t y) { return qcost[x] > qcost[y]; });
+  size_t e = 0;
+  for (size_t g = 0; g < nq; g += 8) {
+    const size_t m = std::min<size_t>(8, nq - g);
+    for (int j = 0; j < group; ++j)
+      for (size_t i = 0; i < m; ++i) {
+        const size_t q = (size_t)qorder[g + i];
+        order[e++] = (int32_t)((q / qx) * (size_t)tiles_x + (q % qx) * (size_t)group + (size_t)j);
+      }
+  }
+}
+
 static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_t band_pitch, uint32_t n_bands,
                         int32_t max_depth, void* out, size_t stride, void* stream, bool f64, bool rgb = false) {
   if (!c || !out) return fail(RT_ERR_INVALID, "null argument");
@@ -308,6 +340,10 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
       }
       h_order.swap(split);
     }
+    const int line_tiles = 128 / (RT_TILE_W * 4);
+    if (max_depth == 0 && !f64 && !rgbi && !slot->deferred && tiles_x % line_tiles == 0 && tstride % 128 == 0 &&
+        ((uintptr_t)target & 127) == 0)
+      xcd_line_order(h_order, h_cost, tiles_x, line_tiles);
     slot->grid = (uint32_t)h_order.size();
     RT_HIP(hipMemcpyAsync(slot->d_order, h_order.data(), h_order.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
     RT_HIP(hipStreamSynchronize(st));

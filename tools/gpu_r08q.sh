@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
-T=${TAG:-r08q}
+T=${TAG:-r08s}
 P=tinyraytracerinrust_amd/librt_mi355x.so
 V=tinyraytracerinrust_amd/build/librt_mi355x_prev.so
 for C in globes4k globes1080d5 sphere1080d0; do
