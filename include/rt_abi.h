@@ -286,7 +286,7 @@ int rt_ctx_synchronize(rt_ctx* ctx);
  * therefore renders as fast as without the option, and the compile (seconds of host time on a new
  * scene; 4K globes: 0.457 -> 0.325 ms per frame once loaded) costs the host thread nothing.
  * rt_ctx_spec_wait blocks for it.  Programs are cached per process by their full text, and on disk
- * (rt_spec_cache_dir) by text and compiler.  Scenes of more than 32 objects or 48 leaves keep the
+ * (rt_spec_cache_dir) by text, compiler, embedded device headers and compile options.  Scenes of more than 32 objects or 48 leaves keep the
  * generic kernels (the unrolled walks grow with the scene), and so does a context whose compile
  * failed or whose code object exceeds the resource guard, or when the ROCm installation's hipRTC
  * cannot be loaded (rt_ctx_kernel_info says why; the upload itself succeeds).  Setting the same
@@ -319,18 +319,22 @@ int rt_scene_precompile(const rt_scene* scene, double* compile_ms);
  * compiler's identity, and per kernel "NAME: vgprs V spilled S sgprs G scratch B occupancy W code N
  * compile_ms T source hiprtc|disk" (the code object's metadata: what the resource guard checks). */
 int rt_scene_spec_report(const rt_scene* scene, char* buf, size_t cap, size_t* len);
-/* The hipRTC the programs compile with (its path, version, real path, size and mtime: the disk-cache
- * key), and *rocm = 1 when it is the ROCm installation's own ($ROCM_PATH or /opt/rocm), loaded into a
+/* The hipRTC the programs compile with (its path, version, real path, size and mtime) and "build H",
+ * H = a hash of the device headers this library embeds and the compile options: together the disk-cache
+ * identity.  *rocm = 1 when it is the ROCm installation's own ($ROCM_PATH or /opt/rocm), loaded into a
  * link-map namespace of its own; 0 when that failed (then nothing is specialised: the process's own
  * hipRTC may be another LLVM -- PyTorch bundles one -- whose code ran 19x slower). */
 int rt_spec_compiler_info(char* buf, size_t cap, int32_t* rocm);
 /* The on-disk code-object cache of the specialised programs: a directory (created on first write);
- * NULL or "" (the default) for none.  Entries are keyed by the full program text and the compiler's
- * identity, and both are compared on a hit. */
+ * NULL or "" (the default) for none.  Entries are keyed by the full program text and the identity of
+ * rt_spec_compiler_info (compiler, embedded headers, options); both are compared on a hit, and the
+ * resources the guard checks are read from the stored code object itself. */
 int rt_spec_cache_dir(const char* dir);
 /* Stop the compile pool before the process exits: queued compiles are cancelled, running ones are
  * waited for (a compile still running in a library thread while the process tears hipRTC down could
- * crash the exit).  Later requests fail (contexts keep the generic kernels). */
+ * crash the exit).  Later requests fail (contexts keep the generic kernels).  The library registers it
+ * with atexit() when its first compile thread starts, so a host that never calls it is covered too;
+ * calling it again is harmless. */
 void rt_spec_shutdown(void);
 /* The specialised program's text (tests, debugging): cap, len as rt_scene_describe. */
 int rt_scene_spec_program(const rt_scene* scene, char* buf, size_t cap, size_t* len);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # anim120 (BASELINE config 5) throughput and HBM traffic per variant library: one bench line and two
-# rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) each.  usage: TAG=x bash tools/anim_variants.sh LIB...
+# rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) each.  usage: TAG=x bash profiles/sessions/anim_variants.sh LIB...
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -163,3 +163,51 @@ print("ok", info)
                          env=dict(os.environ, RT_SPEC_CACHE_DIR=""))
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-3000:]
     assert "ok generic" in res.stdout
+
+
+@pytest.mark.parametrize("case", ["globes_d10", "globes_d5_bands", "globes_f64", "spinning_chain",
+                                  "fuzz_tree", "globes_deferred", "fractal_wavefront"])
+def test_library_default_parity_subset(worldmap, case):
+    """the rest of the suite pins RT_OPT_SPECIALIZE 0 (conftest), so a representative
+    subset runs here with the option as the LIBRARY sets it (specialize=LIBRARY_DEFAULT, i.e. 1), after
+    rt_ctx_spec_wait: whatever kernel the default path then picks -- the specialised megakernel, the
+    deferred or wavefront requests, row bands, f64 rows (generic: option level 1 keeps f64 generic) --
+    every launch (calibration and ordered) is the oracle's, RGBA8 bit-identical / f64 within 1e-9."""
+    import torch
+    import tinyraytracerinrust_amd as T
+    from oracle import oracle as O
+    from tests.scene_fuzz import random_scene
+    W, H, depth, t, kernel = 320, 240, 10, 0.0, None
+    if case.startswith("globes"):
+        text = scene_text("globes")
+        depth = 5 if case == "globes_d5_bands" else 10
+        kernel = "deferred" if case == "globes_deferred" else None
+    elif case == "spinning_chain":
+        text, t = scene_text("spinning_globes"), 0.35
+    elif case == "fuzz_tree":
+        text = random_scene(7773)
+    else:
+        text, W, H, kernel = scene_text("fractal"), 160, 120, "wavefront"
+    osc = O.OracleScene(text, t, W, H, max_depth=depth)
+    ref8 = osc.render(0, H)[1]
+    r = T.Renderer(0, specialize=T.Renderer.LIBRARY_DEFAULT)
+    r.upload(T.Scene.compile(text, t, W, H, asset_dir=SCENES))
+    if kernel:
+        r.set_kernel(kernel)
+    r.spec_wait()
+    for launch in ("calibration", "ordered", "ordered again"):
+        if case == "globes_f64":
+            got = r.render_rows_host(0, H, max_depth=depth, f64=True)
+            ref64 = osc.render(0, H, f64=True)[0]
+            assert np.array_equal(np.isnan(got), np.isnan(ref64))
+            assert np.nanmax(np.abs(got - ref64)) <= 1e-9, f"{case} {launch} ({r.kernel_info()})"
+        elif case == "globes_d5_bands":
+            band, n = 8, H // 8
+            slot = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+            r.render_row_bands(0, band, band, n, slot, max_depth=depth)
+            torch.cuda.synchronize()
+            assert np.array_equal(slot.cpu().numpy(), ref8), f"{case} {launch} ({r.kernel_info()})"
+        else:
+            got = r.render_rows_host(0, H, max_depth=depth)
+            assert np.array_equal(got, ref8), f"{case} {launch}: {int((got != ref8).sum())} channels ({r.kernel_info()})"
+    print(case, r.kernel_info())

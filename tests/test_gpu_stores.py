@@ -98,11 +98,11 @@ def test_split_tiles_4k_share(worldmap):
 
 @pytest.mark.parametrize("W,pad,depth", [(512, 0, 0), (512, 128, 0), (512, 4, 0), (520, 0, 0), (512, 0, 10)])
 def test_cached_frame_stores_and_xcd_order(worldmap, W, pad, depth):
-    """Primary-ray (max_depth 0) RGBA8 frames of at most RT_CACHED_FRAME_BYTES (k_rows.hip) take plain
-    stores through the L2s and, when their rows are whole 128-byte lines (tiles_x % 4 == 0, 128-byte
-    pitch and base), the XCD-aware tile order on ordered launches; other pitches and widths keep the
-    cost order, deeper launches streaming stores.  >= 2048 tiles, so the calibration launch and two
-    ordered launches each give the oracle's bits, padding untouched."""
+    """The XCD-aware line order (k_rows.hip xcd_line_order): ordered primary-ray (max_depth 0) RGBA8
+    launches whose rows are whole 128-byte lines (tiles_x % 4 == 0, 128-byte pitch and base) put a
+    line's four tiles at entries e, e + 8, e + 16, e + 24 of the cost order; other pitches and widths,
+    and deeper launches, keep the plain cost order.  >= 2048 tiles, so the calibration launch and two
+    ordered launches each give the oracle's bits, and the row padding is left untouched."""
     import torch
     H = 256
     text = scene_text("globes")

@@ -161,3 +161,54 @@ def test_family_count_is_bounded():
         raise AssertionError("17+ families accepted")
     except T.RtError as e:
         assert e.status == -6 and "families" in e.message, e.message
+
+
+def _fnv1a(b):
+    h = 1469598103934665603
+    for ch in b:
+        h = ((h ^ ch) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def test_disk_cache_identity_covers_headers_and_options(tmp_path):
+    """the program text only #includes rt_device.h / rt_blob.h / rt_math.h, which the
+    library embeds, so the disk-cache identity must cover them (and the compile options): it ends in
+    "build H" with H = FNV-1a over the three embedded headers and the options, here recomputed from the
+    sources, and an entry written under another build's identity is recompiled, not read."""
+    import subprocess
+    import sys
+    import tinyraytracerinrust_amd as T
+    from tests.conftest import ROOT
+    ident, rocm = T.spec_compiler_info()
+    m = re.search(r" build ([0-9a-f]{16})$", ident)
+    assert m, ident
+    key = b""
+    for h in ("rt_device", "rt_blob", "rt_math"):
+        with open(os.path.join(ROOT, "tinyraytracerinrust_amd", "csrc", h + ".h"), "rb") as f:
+            key += f.read() + b"\0"
+    for o in ("--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-mllvm",
+              "-disable-machine-licm"):
+        key += o.encode() + b"\0"
+    assert int(m.group(1), 16) == _fnv1a(key), "the embedded headers differ from csrc/ (rebuild the library)"
+
+    text = "draw(sphere(<1, 2, 4>, 28.5, green))"          # a program no other test compiles
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import tinyraytracerinrust_amd as T\n"
+            "s = T.Scene.compile(%r, 0.0, 64, 48)\n"
+            "print(s.spec_report())\n" % (ROOT, text))
+    env = dict(os.environ, RT_SPEC_CACHE_DIR=str(tmp_path))
+
+    def run():
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return [l for l in r.stdout.splitlines() if l.startswith("rt_spec_rows_00:")][0]
+    assert "source hiprtc" in run()
+    rows = [f for f in tmp_path.glob("spec_*.rtco") if b"void rt_spec_rows_00(" in f.read_bytes()][0]
+    blob = bytearray(rows.read_bytes())
+    assert blob[:9] == b"RTSPEC03\n"
+    i = blob.find((" build " + m.group(1)).encode())
+    assert i > 0                                           # the entry carries the build identity
+    blob[i + 7] = ord("0") if blob[i + 7] != ord("0") else ord("1")   # another build's headers
+    rows.write_bytes(bytes(blob))
+    assert "source hiprtc" in run()                        # not read: recompiled (and rewritten)
+    assert "source disk" in run()

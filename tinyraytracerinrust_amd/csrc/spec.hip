@@ -493,9 +493,43 @@ void code_resources(SpecCode* c) {
   c->name = mp_value(c->code, ".name", nullptr, &name) ? name : "";
 }
 
-// hipRTC: the program (with the device headers as named headers), the flags the library's own
-// kernels are built with (Makefile HIPFLAGS: -O3, no contraction, no fast-math, MachineLICM off), and
-// the resource use the guard reads from the code object.
+// The hipRTC options: the flags the library's own kernels are built with (Makefile HIPFLAGS: -O3, no
+// contraction, no fast-math, MachineLICM off).
+std::vector<std::string> spec_options() {
+  std::vector<std::string> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                                   "-mllvm", "-disable-machine-licm"};
+#ifdef RT_DIAG_ENV
+  // diagnostic builds: RT_SPEC_OPTS appends options (space-separated) for compiler A/B runs
+  if (const char* e = getenv("RT_SPEC_OPTS")) {
+    std::string s(e), w;
+    for (size_t i = 0; i <= s.size(); ++i)
+      if (i == s.size() || s[i] == ' ') { if (!w.empty()) opts.push_back(w); w.clear(); } else w += s[i];
+  }
+#endif
+  return opts;
+}
+
+// The disk-cache identity of a code object: the compiler's (rtc().identity) plus a hash of everything
+// else the object depends on besides the program text -- the device headers this library embeds (the
+// text only #includes them) and the compile options.  A rebuild that changes a header (a record layout,
+// a kernel argument) changes the identity, so an entry written by another build is never read.
+std::string spec_build_identity() {
+  std::string key;
+  for (const char* h : {spec_hdr_rt_device, spec_hdr_rt_blob, spec_hdr_rt_math}) {
+    key += h;
+    key += '\0';
+  }
+  for (const std::string& o : spec_options()) {
+    key += o;
+    key += '\0';
+  }
+  char buf[40];
+  snprintf(buf, sizeof buf, " build %016llx", (unsigned long long)fnv1a(key));
+  return rtc().identity + buf;
+}
+
+// hipRTC: the program (with the device headers as named headers), spec_options(), and the resource use
+// the guard reads from the code object.
 int spec_compile(const std::string& src, SpecCode* out, std::string* err) {
   const char* headers[] = {spec_hdr_rt_device, spec_hdr_rt_blob, spec_hdr_rt_math};
   const char* names[] = {"rt_device.h", "rt_blob.h", "rt_math.h"};
@@ -505,18 +539,9 @@ int spec_compile(const std::string& src, SpecCode* out, std::string* err) {
     *err = "hiprtcCreateProgram failed";
     return RT_ERR_DEVICE;
   }
-  std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                                   "-mllvm", "-disable-machine-licm"};
-#ifdef RT_DIAG_ENV
-  // diagnostic builds: RT_SPEC_OPTS appends options (space-separated) for compiler A/B runs
-  std::vector<std::string> extra;
-  if (const char* e = getenv("RT_SPEC_OPTS")) {
-    std::string s(e), w;
-    for (size_t i = 0; i <= s.size(); ++i)
-      if (i == s.size() || s[i] == ' ') { if (!w.empty()) extra.push_back(w); w.clear(); } else w += s[i];
-  }
-  for (const std::string& x : extra) opts.push_back(x.c_str());
-#endif
+  const std::vector<std::string> ostr = spec_options();
+  std::vector<const char*> opts;
+  for (const std::string& x : ostr) opts.push_back(x.c_str());
   const auto t0 = std::chrono::steady_clock::now();
   const hiprtcResult r = R.compile(prog, (int)opts.size(), opts.data());
   out->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -567,8 +592,9 @@ int spec_guard(const SpecCode& c, const std::string& text, std::string* err) {
   return RT_OK;
 }
 
-// On-disk cache entry: "RTSPEC02\n", then length-prefixed (u64) compiler identity, program text, kernel
-// name and code object, and the five resource numbers (i32).  A hit must match identity AND text.
+// On-disk cache entry: "RTSPEC03\n", then length-prefixed (u64) identity (spec_build_identity), program
+// text, kernel name and code object.  A hit must match identity AND text; the resource numbers the guard
+// checks are read from the code object itself (code_resources), never from the file.
 void put_blob(std::string& f, const void* p, uint64_t n) {
   f.append((const char*)&n, 8);
   f.append((const char*)p, n);
@@ -596,18 +622,16 @@ bool disk_read(const std::string& path, const std::string& identity, const std::
   size_t n;
   while ((n = fread(buf, 1, sizeof buf, fi)) > 0) f.insert(f.end(), buf, buf + n);
   fclose(fi);
-  static const char magic[] = "RTSPEC02\n";
+  static const char magic[] = "RTSPEC03\n";
   if (f.size() < 9 || memcmp(f.data(), magic, 9) != 0) return false;
   size_t at = 9;
   std::string id, tx, name, code;
   if (!get_blob(f, &at, &id) || id != identity || !get_blob(f, &at, &tx) || tx != text || !get_blob(f, &at, &name) ||
-      !get_blob(f, &at, &code) || at + 20 > f.size())
+      !get_blob(f, &at, &code) || at != f.size())
     return false;
-  int v[5];
-  memcpy(v, f.data() + at, 20);
-  out->name = name;
   out->code.assign(code.begin(), code.end());
-  out->vgprs = v[0]; out->sgprs = v[1]; out->scratch = v[2]; out->vspill = v[3]; out->occupancy = v[4];
+  code_resources(out);                                    // name and resources from the code object's metadata
+  if (out->name != name) return false;
   out->compile_ms = 0.0;
   out->from_disk = true;
   return true;
@@ -616,13 +640,11 @@ void disk_write(const std::string& dir, const std::string& path, const std::stri
                 const SpecCode& c) {
   for (size_t i = 1; i <= dir.size(); ++i)              // mkdir -p
     if (i == dir.size() || dir[i] == '/') (void)mkdir(dir.substr(0, i).c_str(), 0755);
-  std::string f("RTSPEC02\n");
+  std::string f("RTSPEC03\n");
   put_blob(f, identity.data(), identity.size());
   put_blob(f, text.data(), text.size());
   put_blob(f, c.name.data(), c.name.size());
   put_blob(f, c.code.data(), c.code.size());
-  const int v[5] = {c.vgprs, c.sgprs, c.scratch, c.vspill, c.occupancy};
-  f.append((const char*)v, 20);
   char tmp[64];
   snprintf(tmp, sizeof tmp, ".tmp.%d.%llx", (int)getpid(), (unsigned long long)std::hash<std::thread::id>()(std::this_thread::get_id()));
   const std::string tp = path + tmp;
@@ -646,11 +668,12 @@ int spec_obtain(const std::string& text, SpecCode* out, std::string* err) {
     std::lock_guard<std::mutex> lk(g_spec_mu);
     dir = sst().disk_dir;
   }
-  const std::string path = dir.empty() ? "" : disk_path(dir, R.identity, text);
-  if (!path.empty() && disk_read(path, R.identity, text, out)) return spec_guard(*out, text, err);
+  const std::string ident = dir.empty() ? "" : spec_build_identity();
+  const std::string path = dir.empty() ? "" : disk_path(dir, ident, text);
+  if (!path.empty() && disk_read(path, ident, text, out)) return spec_guard(*out, text, err);
   int rc = spec_compile(text, out, err);
   if (!rc) rc = spec_guard(*out, text, err);
-  if (!rc && !path.empty()) disk_write(dir, path, R.identity, text, *out);
+  if (!rc && !path.empty()) disk_write(dir, path, ident, text, *out);
   return rc;
 }
 
@@ -714,7 +737,14 @@ std::shared_ptr<SpecJob> spec_request(const std::string& text, bool retry = fals
   }
   S.queue.push_back(j);
   const size_t want = std::min<size_t>(RT_SPEC_WORKERS_MAX, std::max(1u, std::thread::hardware_concurrency()));
-  if (S.workers.size() < want) S.workers.emplace_back(spec_worker);
+  if (S.workers.size() < want) {
+    // A host that exits while a compile runs would tear down hipRTC / LLVM under a live worker: the
+    // first worker registers rt_spec_shutdown at exit (it waits for running compiles, cancels queued
+    // ones), so every host is covered, not only the Python wrapper (which also calls it).
+    static std::once_flag at_exit;
+    std::call_once(at_exit, [] { atexit(rt_spec_shutdown); });
+    S.workers.emplace_back(spec_worker);
+  }
   S.qcv.notify_one();
   return job_token(j);
 }
@@ -1061,7 +1091,7 @@ extern "C" int rt_spec_cache_dir(const char* dir) {
 extern "C" int rt_spec_compiler_info(char* buf, size_t cap, int32_t* rocm) {
   const Rtc& R = rtc();
   if (rocm) *rocm = R.rocm ? 1 : 0;
-  if (buf && cap > 0) snprintf(buf, cap, "%s", R.identity.c_str());
+  if (buf && cap > 0) snprintf(buf, cap, "%s", spec_build_identity().c_str());
   return RT_OK;
 }
 
