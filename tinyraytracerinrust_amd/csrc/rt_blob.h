@@ -29,6 +29,11 @@ using __hip_internal::uint64_t;
 
 #define RT_EPSILON 10e-7            /* math.rs:2 */
 #define RT_CULL_COORD_MAX 1e6        /* culling boxes / ray origins beyond this are never culled */
+/* f32 culling (rt_device.h fbox_may_hit): rays whose origin has a coordinate beyond RT_CULL32_COORD_MAX
+ * are never culled; every f32 box is the f64 box grown by RT_CULL32_MARGIN = RT_CULL32_COORD_MAX * 2^-22
+ * (4x the rounding of an origin coordinate to f32) and then rounded outward to f32 (scene.cpp). */
+#define RT_CULL32_COORD_MAX 65536.0
+#define RT_CULL32_MARGIN (RT_CULL32_COORD_MAX / 4194304.0)
 #define RT_MAX_DEPTH_CAP 16          /* recursion frames kept per lane (max_depth <= 16) */
 #define RT_MAX_LITS 4                /* inline hit-filter literals per leaf */
 
@@ -92,6 +97,8 @@ struct alignas(16) RtLeaf {
   int32_t lit[RT_MAX_LITS];   // literal = 2 * leaf + want: leaf[lit >> 1].is_inside(p) == (lit & 1)
   int32_t object;       // the top-level object this leaf belongs to (the cooperative tail walk, rt_device.h)
   int32_t pad0[2];
+  float fblo[3], fbhi[3]; // blo / bhi as the f32 culling box (RT_CULL32_MARGIN, rounded outward)
+  int32_t pad1[2];
   double blo[3], bhi[3];// culling box of this leaf's accepted hits (own bound ^ required-inside siblings)
   double inv[12];       // inverse matrix rows 0..2 (row-major, 4 per row)
   double inv_o[3];      // transform_vector((0,0,0), inverse)   (transformation.rs:80-83)
@@ -158,6 +165,8 @@ struct alignas(16) RtObject {
                                     // region, whose box in the leaf's OWN frame (olo, ohi) is much
                                     // tighter than blo/bhi (rotated thin rods and slabs); -1: none
   double olo[3], ohi[3];            // that box in obb_leaf's object space, inflated (scene.cpp obb)
+  float folo[3], fohi[3];           // olo / ohi as the f32 culling box (RT_CULL32_MARGIN, rounded outward)
+  int32_t pad1[2];
 };
 
 // Order-preserving object hierarchy: a pre-order list of nodes over CONTIGUOUS runs of objects
@@ -170,6 +179,8 @@ struct alignas(16) RtTrav {
   int32_t skip;                     // node index after this node's subtree
   int32_t cull;                     // object node: a copy of RtObject::cull (one record per step of a
   int32_t shadow_skip;              //   per-lane walk, k_wavefront.hip wfp_cand_kernel), ::shadow_skip
+  float fblo[3], fbhi[3];           // blo / bhi as the f32 culling box (RT_CULL32_MARGIN, rounded outward)
+  int32_t pad0[2];
 };
 
 struct RtTexture {

@@ -501,6 +501,69 @@ template <class P> __device__ __forceinline__ bool box_may_hit(P lo, P hi, const
 }
 __device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) + 1e-7; }
 
+// The same test in f32 (RT_CULL_F32, the traversals of the megakernels and the deferred kernel): half
+// the registers of the f64 culling ray, f32 instructions at twice the f64 issue rate, and the box
+// bounds as 32-bit literals (VOP2 operands) in the specialised programs.  Conservative by construction:
+//  * a ray is culled only if every origin coordinate is within RT_CULL32_COORD_MAX and its largest
+//    direction component within [2^-10, 2^10] (cull_ray_f; otherwise every slab time is NaN, which
+//    narrows nothing: min/max are IEEE minNum/maxNum);
+//  * the f32 boxes are the f64 boxes grown by RT_CULL32_MARGIN = 4x the error of rounding such an origin
+//    to f32, then rounded outward (scene.cpp f32_boxes), so the slab times computed from the rounded
+//    origin bound those of the exact origin against a box that still contains the f64 box;
+//  * what remains is relative: fl32(box - o) * rcp32(fl32(d)) is within 2^-21 of its exact value, and
+//    the comparison tn <= tf allows 2^-18 of slack on each side;
+//  * a direction component below 2^-100 is taken as zero (inv = +-inf): reaching a slab RT_CULL32_MARGIN
+//    away would take t > 2^93, where the largest component (>= 2^-10) has left every box (|bounds| <= 1e6);
+//    (box - o) * inf is +-inf, or NaN (narrows nothing) when box - o == 0;
+//  * the only infinite time that reaches the comparison is tn = +inf from such a zero component with
+//    the origin outside its slab (the ray never enters it: exact), and tf is finite (some component
+//    is >= 2^-10), so the slack never hides an infinity.
+#ifndef RT_CULL_F32
+#define RT_CULL_F32 1
+#endif
+struct CullRayF { float ox, oy, oz, ix, iy, iz; };
+__device__ __forceinline__ float cull_rcp_f(float x) {
+  return fabsf(x) < 0x1p-100f ? copysignf(__builtin_inff(), x) : __builtin_amdgcn_rcpf(x);
+}
+__device__ __forceinline__ CullRayF cull_ray_f(V3 o, V3 d) {
+  const double ad = fmax(fmax(fabs(d.x), fabs(d.y)), fabs(d.z));
+  const bool ok = fabs(o.x) <= RT_CULL32_COORD_MAX && fabs(o.y) <= RT_CULL32_COORD_MAX &&
+                  fabs(o.z) <= RT_CULL32_COORD_MAX && ad >= 0x1p-10 && ad <= 0x1p10;
+  const float nan = __builtin_nanf("");
+  return {(float)o.x, (float)o.y, (float)o.z, ok ? cull_rcp_f((float)d.x) : nan, ok ? cull_rcp_f((float)d.y) : nan,
+          ok ? cull_rcp_f((float)d.z) : nan};
+}
+template <class P> __device__ __forceinline__ bool fbox_may_hit(P lo, P hi, const CullRayF& r, float tmax) {
+  const float ax = (lo[0] - r.ox) * r.ix, bx = (hi[0] - r.ox) * r.ix;
+  const float ay = (lo[1] - r.oy) * r.iy, by = (hi[1] - r.oy) * r.iy;
+  const float az = (lo[2] - r.oz) * r.iz, bz = (hi[2] - r.oz) * r.iz;
+  const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+  const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
+  return tn * (1.0f - 0x1p-18f) <= __builtin_fmaf(fabsf(tf), 0x1p-18f, tf);
+}
+__device__ __forceinline__ float cull_tmax_f(double t) { return (float)cull_tmax(t); }
+#if RT_CULL_F32
+// The traversals' culling ray and tests, f32 (above) or f64 (box_may_hit)
+typedef CullRayF CullR;
+typedef float CullT;
+#define RT_CULL_RAY(o, d) cull_ray_f(o, d)
+#define RT_CULL_TMAX(t) cull_tmax_f(t)
+#define RT_BOX_MAY_HIT(R, lo, hi, cr, tm) fbox_may_hit((R)->f##lo, (R)->f##hi, cr, tm)
+#else
+typedef CullRay CullR;
+typedef double CullT;
+#define RT_CULL_RAY(o, d) cull_ray(o, d)
+#define RT_CULL_TMAX(t) cull_tmax(t)
+#define RT_BOX_MAY_HIT(R, lo, hi, cr, tm) box_may_hit((R)->lo, (R)->hi, cr, tm)
+#endif
+// The range the host proves constant hit filters for (RtLeaf::filter_const): cull_ray's valid range
+// (origin within 1e6, largest direction component within [1e-100, 1e100]).
+__device__ __forceinline__ bool const_filter_range(V3 o, V3 d) {
+  const double ad = fmax(fmax(fabs(d.x), fabs(d.y)), fabs(d.z));
+  return fabs(o.x) <= RT_CULL_COORD_MAX && fabs(o.y) <= RT_CULL_COORD_MAX && fabs(o.z) <= RT_CULL_COORD_MAX &&
+         ad >= 1e-100 && ad <= 1e100;
+}
+
 // The object's oriented box (RtObject::obb_leaf, scene.cpp obb): may the segment t in [0, tmax]
 // meet the leaf-frame box olo/ohi?  The ray is taken to the leaf's frame with the leaves' own
 // arithmetic; outside the range the host's margins are proven for (|o| <= 1e6, unit-length
@@ -510,13 +573,13 @@ __device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) 
 #ifndef RT_OBB
 #define RT_OBB 1
 #endif
-__device__ __forceinline__ bool obb_may_hit(const DS& S, cptr<RtObject> O, V3 ro, V3 rd, double tmax) {
+__device__ __forceinline__ bool obb_may_hit(const DS& S, cptr<RtObject> O, V3 ro, V3 rd, CullT tmax) {
   RT_REC(R, S, leaves, LEAVES, O->obb_leaf);
   const double ad = fmax(fmax(fabs(rd.x), fabs(rd.y)), fabs(rd.z));
   if (!(ad >= 0.25 && ad <= 4.0 && fabs(ro.x) <= 1e6 && fabs(ro.y) <= 1e6 && fabs(ro.z) <= 1e6)) return true;
   const V3 o = xf(R->inv, ro);
   const V3 d = sub(xf(R->inv, rd), ld3(R->inv_o));
-  return box_may_hit(O->olo, O->ohi, cull_ray(o, d), tmax);
+  return RT_BOX_MAY_HIT(O, olo, ohi, RT_CULL_RAY(o, d), tmax);   // leaf-frame ray: cull_ray*'s own range checks
 }
 
 // ------------------------------------------------------------------ traversal (raytracer.rs)
@@ -602,33 +665,34 @@ RT_FN int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist) {
   double best = INFINITY;
   int bobj = -1;
   SphereShare shr = {0.0, 0.0, 0.0};
-  const CullRay cr = cull_ray(ro, rd);
+  const CullR cr = RT_CULL_RAY(ro, rd);
+  const bool cf_ok = SHARE && RT_CONST_FILTER && const_filter_range(ro, rd);
   const bool fin = wave_finite(ro, rd);
   // NORDER (reflection-only kernels): the objects in S.strav's order, largest regions first, so an
   // early hit on a big object culls what lies behind it.  Exact: a candidate equal to the best
   // distance so far wins when its object comes earlier in DRAW order (o < bobj), which is the
   // reference's first-visited-wins rule (raytracer.rs:141-150) for any visiting order.
   constexpr bool NORDER = RT_NEAREST_ORDER && OBB;
-  auto group = [&](cptr<RtTrav> T) RT_INL { return box_may_hit(T->blo, T->bhi, cr, cull_tmax(best)); };
+  auto group = [&](cptr<RtTrav> T) RT_INL { return RT_BOX_MAY_HIT(T, blo, bhi, cr, RT_CULL_TMAX(best)); };
   auto object = [&](cptr<RtTrav> T) RT_INL {
     // the object's cull kind and box come from the node's copy (RtTrav): one scalar load for the
     // node decides the common case; the object's own record is read only once its box passes
     if (T->cull == RT_CULL_ALWAYS) return;
-    if (T->cull == RT_CULL_BOX && !box_may_hit(T->blo, T->bhi, cr, cull_tmax(best))) return;
+    if (T->cull == RT_CULL_BOX && !RT_BOX_MAY_HIT(T, blo, bhi, cr, RT_CULL_TMAX(best))) return;
     const int o = T->obj;
     RT_REC(O, S, objects, OBJECTS, o);
-    if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, ro, rd, cull_tmax(best))) return;
+    if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, ro, rd, RT_CULL_TMAX(best))) return;
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
     RT_SPEC_UNROLL
     for (int l = lb; l < le; ++l) {
       RT_REC(L, S, leaves, LEAVES, l);
       if (O->leaf_cull) {
         if (L->cull == RT_CULL_ALWAYS) continue;
-        if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, cull_tmax(best))) continue;
+        if (L->cull == RT_CULL_BOX && !RT_BOX_MAY_HIT(L, blo, bhi, cr, RT_CULL_TMAX(best))) continue;
       }
       double t0 = 0.0, t1 = 0.0;
       int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1, SHARE ? &shr : nullptr);
-      const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && SHARE && L->filter_const && !isnan(cr.inv.x));
+      const bool filtered = L->prog_end != L->prog_begin && !(cf_ok && L->filter_const);
       if (n >= 1 && t0 > EPS && (t0 < best || (NORDER && t0 == best && o < bobj)) &&
           (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) {
         best = t0; bobj = o;
@@ -659,14 +723,15 @@ RT_FN double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
   double tr = 1.0;
   bool done = false;
   SphereShare shr = {0.0, 0.0, 0.0};
-  const CullRay cr = cull_ray(p, dir);
+  const CullR cr = RT_CULL_RAY(p, dir);
+  const bool cf_ok = SHARE && RT_CONST_FILTER && const_filter_range(p, dir);
   const bool fin = wave_finite(p, dir);
-  const double tmax = cull_tmax(dist);
-  auto group = [&](cptr<RtTrav> T) RT_INL { return !done && box_may_hit(T->blo, T->bhi, cr, tmax); };
+  const CullT tmax = RT_CULL_TMAX(dist);
+  auto group = [&](cptr<RtTrav> T) RT_INL { return !done && RT_BOX_MAY_HIT(T, blo, bhi, cr, tmax); };
   auto object = [&](cptr<RtTrav> T) RT_INL {
     if (done) return;
     if (T->shadow_skip || T->cull == RT_CULL_ALWAYS) return;     // the node's copies (see nearest_hit)
-    if (T->cull == RT_CULL_BOX && !box_may_hit(T->blo, T->bhi, cr, tmax)) return;
+    if (T->cull == RT_CULL_BOX && !RT_BOX_MAY_HIT(T, blo, bhi, cr, tmax)) return;
     RT_REC(O, S, objects, OBJECTS, T->obj);
     if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, p, dir, tmax)) return;
     const double tobj = O->transparency;
@@ -676,11 +741,11 @@ RT_FN double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
       RT_REC(L, S, leaves, LEAVES, l);
       if (O->leaf_cull) {
         if (L->cull == RT_CULL_ALWAYS) continue;
-        if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
+        if (L->cull == RT_CULL_BOX && !RT_BOX_MAY_HIT(L, blo, bhi, cr, tmax)) continue;
       }
       double t0 = 0.0, t1 = 0.0;
       int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1, SHARE ? &shr : nullptr);
-      const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && SHARE && L->filter_const && !isnan(cr.inv.x));
+      const bool filtered = L->prog_end != L->prog_begin && !(cf_ok && L->filter_const);
       if (n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) {
         tr *= tobj;
         if (tr == 0.0 && S.shadow_early_out) { done = true; return; }

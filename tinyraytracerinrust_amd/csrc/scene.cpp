@@ -710,6 +710,34 @@ std::string describe_flat(const FlatScene& f) {
   return s;
 }
 
+// ---------------------------------------------------------------- f32 culling boxes
+// The kernels' culling slab tests run in f32 (rt_device.h fbox_may_hit): every box is grown by
+// RT_CULL32_MARGIN and rounded outward to f32, so the f32 box contains the f64 one plus a margin four
+// times the rounding of any culled ray's origin (|o| <= RT_CULL32_COORD_MAX) to f32.  Boxes that are
+// never tested (cull NONE / ALWAYS) get +-inf; the f64 boxes stay for the wavefront path.
+static float f32_down(double x) {
+  float v = (float)(x - RT_CULL32_MARGIN);
+  if ((double)v > x - RT_CULL32_MARGIN) v = nextafterf(v, -INFINITY);
+  return v;
+}
+static float f32_up(double x) {
+  float v = (float)(x + RT_CULL32_MARGIN);
+  if ((double)v < x + RT_CULL32_MARGIN) v = nextafterf(v, INFINITY);
+  return v;
+}
+static void f32_box(const double* lo, const double* hi, bool tested, float* flo, float* fhi) {
+  for (int i = 0; i < 3; ++i) {
+    flo[i] = tested ? f32_down(lo[i]) : -INFINITY;
+    fhi[i] = tested ? f32_up(hi[i]) : INFINITY;
+  }
+}
+static void f32_boxes(FlatScene& f) {
+  for (RtLeaf& L : f.leaves) f32_box(L.blo, L.bhi, L.cull == RT_CULL_BOX, L.fblo, L.fbhi);
+  for (RtObject& o : f.objects) f32_box(o.olo, o.ohi, o.obb_leaf >= 0, o.folo, o.fohi);
+  for (std::vector<RtTrav>* tv : {&f.trav, &f.strav})
+    for (RtTrav& t : *tv) f32_box(t.blo, t.bhi, t.obj < 0 || t.cull == RT_CULL_BOX, t.fblo, t.fbhi);
+}
+
 int flatten(const rt_scene& s, FlatScene* out) {
   FlatScene& f = *out;
   f = FlatScene();
@@ -829,6 +857,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
     build_hierarchy(&f, draw, &f.trav);
     build_hierarchy(&f, shadow_order(f), &f.strav);
   }
+  f32_boxes(f);
   for (const LightRec& l : s.lights) {
     RtLight L;
     for (int i = 0; i < 3; ++i) { L.p[i] = l.p[i]; L.col[i] = l.color[i]; }
