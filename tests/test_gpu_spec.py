@@ -69,8 +69,9 @@ def test_globes4k_rank_bands_specialised(worldmap, world):
 
 def test_sphere1080_d0_specialised_full_frame():
     """BASELINE config 2 as `bench.py --config sphere1080d0` runs it (RT_OPT_SPECIALIZE 1, timing
-    events off): the calibration launch and the cost-ordered launches of the specialised megakernel,
-    1920x1080 primary rays only, every pixel against the oracle."""
+    events off): the calibration launch and the cost-ordered launches of the specialised primary-ray
+    kernel (rt_spec_prim_00: max_depth 0 at compile time, write-back stores, XCD line order), 1920x1080
+    primary rays only, every pixel against the oracle."""
     import torch
     W, H = 1920, 1080
     text = "draw(sphere(<0, 0, 0>, 30, red))"
@@ -82,7 +83,40 @@ def test_sphere1080_d0_specialised_full_frame():
         torch.cuda.synchronize()
         info = r.kernel_info()
         assert_close(f.cpu().numpy(), None, ref, None, f"spec sphere 1080p d0 {launch} launch ({info})")
-    assert "megakernel (specialised)" in info, info
+    assert "primary-ray (specialised)" in info, info
+
+
+@pytest.mark.parametrize("scene,t,level", [("globes", 0.0, 1), ("globes", 0.3, 2), ("spinning_globes", 0.45, 1),
+                                           ("fuzz_tree", 0.0, 1), ("fuzz_tree", 0.0, 2)])
+def test_primary_ray_kernel_every_mode(worldmap, scene, t, level):
+    """The primary-ray kernel of every kernel mode (reflection-only, refraction chains, ray trees) for
+    max_depth 0 launches: calibration and ordered launches (level 2: the calibration launch is the
+    primary-ray kernel's CAL form, and f64 rows too), full frames and row bands, against the oracle."""
+    import torch
+    from tests.scene_fuzz import random_scene
+    from tinyraytracerinrust_amd import distributed as D
+    W, H = 640, 360
+    text = random_scene(7774) if scene == "fuzz_tree" else scene_text(scene)
+    rt, r = _renderer(text, t, W, H, 0, level)
+    f64ref, ref = _oracle(text, t, W, H, 0, f64=level == 2)
+    for launch in ("calibration", "ordered"):
+        f = r.render_rows(0, H, max_depth=0)
+        torch.cuda.synchronize()
+        info = r.kernel_info()
+        assert_close(f.cpu().numpy(), None, ref, None, f"prim {scene} {launch} ({info})")
+        assert launch == "calibration" and level == 1 or "primary-ray (specialised)" in info, info
+    if level == 2:
+        got = r.render_rows_host(0, H, max_depth=0, f64=True)
+        assert "primary-ray (specialised)" in r.kernel_info(), r.kernel_info()
+        assert np.nanmax(np.abs(got - f64ref)) <= 1e-9 and np.array_equal(np.isnan(got), np.isnan(f64ref))
+    world = 4
+    slot_rows = D.rows_per_rank(H, world, "cyclic", 8)
+    gath = torch.zeros((world * slot_rows, W, 3), dtype=torch.uint8, device="cuda")
+    for rank in range(world):
+        y_first, band_rows, pitch, n_bands = D.band_params(H, world, rank, "cyclic", 8)
+        r.render_row_bands(y_first, band_rows, pitch, n_bands, gath[rank * slot_rows:(rank + 1) * slot_rows], max_depth=0)
+    frame = D.assemble(gath, H, world, "cyclic", 8).cpu().numpy()
+    assert np.array_equal(frame[..., :3], ref[..., :3]), f"prim {scene} bands"
 
 
 @pytest.mark.parametrize("kernel", ["auto", "deferred", "mega"])

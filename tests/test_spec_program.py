@@ -30,7 +30,7 @@ def test_program_holds_the_flattened_tables():
         obj, skip = struct.unpack("<ii", struct.pack("<Q", w[6]))
         assert (obj, skip) == (o, k)
     # reflection-only scene: megakernel and deferred kernels, f64 and calibration forms
-    for k in ("rt_spec_rows_00", "rt_spec_rows_11", "rt_spec_def_00", "rt_spec_def_11"):
+    for k in ("rt_spec_rows_00", "rt_spec_rows_11", "rt_spec_def_00", "rt_spec_def_11", "rt_spec_prim_00", "rt_spec_prim_11"):
         assert f"void {k}(" in prog
     # a refraction-chain scene has no deferred kernels in its program
     assert "rt_spec_def_" not in _scene(scene_text("spinning_globes"), 0.3).spec_program()
@@ -114,7 +114,8 @@ def test_guard_bounds_hold_for_the_benchmark_programs():
     globes.scene's megakernel and deferred kernel -- and reports what hipRTC built."""
     comp, ks = _report(scene_text("globes"))
     assert "ROCm installation" in comp, comp
-    assert set(ks) == {"rt_spec_rows_00", "rt_spec_def_00"}, ks
+    assert set(ks) == {"rt_spec_rows_00", "rt_spec_def_00", "rt_spec_prim_00"}, ks
+    assert int(ks["rt_spec_prim_00"]["scratch"]) == 0         # no frame stack in the primary-ray kernel
     assert int(ks["rt_spec_rows_00"]["vgprs"]) <= 128 and int(ks["rt_spec_rows_00"]["scratch"]) <= 1024
     assert int(ks["rt_spec_def_00"]["scratch"]) <= 2048
 
@@ -139,7 +140,7 @@ def test_disk_cache_keyed_and_checked_by_text(tmp_path):
         return [l for l in r.stdout.splitlines() if l.startswith("rt_spec_rows_00:")][0]
     assert "source hiprtc" in run()
     files = list(tmp_path.glob("spec_*.rtco"))
-    assert len(files) == 2                                 # a reflection-only scene: megakernel + deferred kernel
+    assert len(files) == 3                                 # a reflection-only scene: megakernel, deferred, primary-ray
     assert "source disk" in run()                          # another process: from the disk cache
     rows = [f for f in files if b"void rt_spec_rows_00(" in f.read_bytes()][0]
     blob = bytearray(rows.read_bytes())

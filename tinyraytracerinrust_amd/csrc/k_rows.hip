@@ -241,9 +241,17 @@ static int launch_bands(rt_ctx* c, uint32_t y_first, uint32_t band_rows, uint32_
   const int mode = chain ? RT_MODE_CHAIN : refr ? RT_MODE_TREE : RT_MODE_REFL;
   // the scene-specialised kernel of this launch (spec.hip), when the context holds one that matches
   hipFunction_t sfn = nullptr;
-  if (c->spec_mod && mode == c->spec_mode && fc == c->spec_fc)
-    sfn = deferred ? c->spec_def[f64 ? 1 : 0][calibrate ? 1 : 0] : c->spec_rows[f64 ? 1 : 0][calibrate ? 1 : 0];
-  c->last_kernel = deferred ? (sfn ? "deferred (specialised)" : "deferred") : (sfn ? "megakernel (specialised)" : "megakernel");
+  bool prim = false;
+  if (c->spec_mod && mode == c->spec_mode && fc == c->spec_fc) {
+    // launches of primary rays only (max_depth 0) take the program's primary-ray kernel (no frame stack,
+    // rt_device.h PRIM) unless the deferred kernel was asked for
+    prim = max_depth == 0 && dmode != 1 && c->spec_prim[f64 ? 1 : 0][calibrate ? 1 : 0];
+    if (prim) deferred = false;
+    sfn = prim ? c->spec_prim[f64 ? 1 : 0][calibrate ? 1 : 0]
+               : deferred ? c->spec_def[f64 ? 1 : 0][calibrate ? 1 : 0] : c->spec_rows[f64 ? 1 : 0][calibrate ? 1 : 0];
+  }
+  c->last_kernel = prim ? "primary-ray (specialised)"
+                        : deferred ? (sfn ? "deferred (specialised)" : "deferred") : (sfn ? "megakernel (specialised)" : "megakernel");
   if (sfn) {
     void* kargs[] = {&c->dev, (void*)&a0, (void*)&a1, (void*)&a2, (void*)&a3, &max_depth, &target, &tstride,
                      (void*)&order, &cost, (void*)&rgbi};

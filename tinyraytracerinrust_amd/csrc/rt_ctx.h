@@ -75,9 +75,10 @@ struct rt_ctx {
   bool spec_deferred = false;           // the program also holds the deferred kernels
   bool spec_fits = false;               // small enough to specialise (RT_SPEC_MAX_OBJECTS / _LEAVES)
   hipModule_t spec_mod = nullptr;       // non-null once the kernels are loaded (null: generic kernels)
-  hipModule_t spec_mods[8] = {};        // one module per specialised kernel, on this context's device
+  hipModule_t spec_mods[12] = {};       // one module per specialised kernel, on this context's device
   hipFunction_t spec_rows[2][2] = {};   // [f64][cal]
   hipFunction_t spec_def[2][2] = {};    // [f64][cal]
+  hipFunction_t spec_prim[2][2] = {};   // [f64][cal]: the primary-ray kernel (max_depth 0 launches)
   uint64_t spec_hash = 0;               // FNV-1a of the prelude (kernel info only; caches compare full texts)
   double spec_compile_ms = 0.0;         // the hipRTC time of the loaded programs (0: read from the disk cache)
   int spec_family = 0;                  // > 0: the program of a registered scene family of that many members

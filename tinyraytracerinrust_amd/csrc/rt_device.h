@@ -1475,26 +1475,28 @@ __device__ __forceinline__ int band_row(int r, int y_first, int band_rows, int b
 // reached memory as its own partial-line write-back: WRITE_SIZE counted 118 MiB for a 31.6 MiB
 // background-only 4K frame, 71 MiB with streaming stores, at equal kernel time
 // (profiles/r06h_nt_stores.txt).  Diagnostic builds with RT_PLAIN_STORES keep plain stores.
-template <class T>
+// PLAIN: write-back stores (the primary-ray kernels, below).
+template <bool PLAIN = false, class T>
 __device__ __forceinline__ void frame_store(T v, T* p) {
 #ifdef RT_PLAIN_STORES
   *p = v;
 #else
-  __builtin_nontemporal_store(v, p);
+  if constexpr (PLAIN) *p = v;
+  else __builtin_nontemporal_store(v, p);
 #endif
 }
-template <bool F64>
+template <bool F64, bool PLAIN = false>
 __device__ __forceinline__ void store_pixel(uint8_t* row, int x, Col c, int rgb) {
   if constexpr (F64) {
     double* o = (double*)row + (size_t)x * 4;
     o[0] = c.r; o[1] = c.g; o[2] = c.b; o[3] = 1.0;
   } else if (rgb) {
     uint8_t* o = row + (size_t)x * 3;
-    frame_store((uint8_t)to_u8(c.r), o);
-    frame_store((uint8_t)to_u8(c.g), o + 1);
-    frame_store((uint8_t)to_u8(c.b), o + 2);
+    frame_store<PLAIN>((uint8_t)to_u8(c.r), o);
+    frame_store<PLAIN>((uint8_t)to_u8(c.g), o + 1);
+    frame_store<PLAIN>((uint8_t)to_u8(c.b), o + 2);
   } else {
-    frame_store(to_u8(c.r) | (to_u8(c.g) << 8) | (to_u8(c.b) << 16) | (255u << 24), (uint32_t*)row + x);
+    frame_store<PLAIN>(to_u8(c.r) | (to_u8(c.g) << 8) | (to_u8(c.b) << 16) | (255u << 24), (uint32_t*)row + x);
   }
 }
 
@@ -1534,15 +1536,20 @@ template <int MODE, int KL_ = -1>
 constexpr int rows_lane_frames() {
   return KL_ >= 0 ? KL_ : MODE == RT_MODE_CHAIN ? RT_LDS_FRAMES_CHAIN : RT_LDS_FRAMES;
 }
-template <int MODE, bool F64, bool CAL, bool FC, int KL_ = -1, int KP_ = -1>
+// PRIM (the primary-ray kernels of the specialised programs, launches with max_depth 0): max_depth is the
+// compile-time 0, so trace() never pushes a frame -- no frame stack, no LDS, no bounce loop -- and the
+// frame takes write-back stores (such launches order their tiles by 128-byte line and XCD, k_rows.hip
+// xcd_line_order, so a line's four tiles are written back to back through one L2).
+template <int MODE, bool F64, bool CAL, bool FC, int KL_ = -1, int KP_ = -1, bool PRIM = false>
 __device__ __forceinline__ void rows_entry(const RtDevScene& S, unsigned entry, int y_first, int band_rows, int band_pitch,
                                            int n_rows, int max_depth, uint8_t* __restrict__ out, size_t stride,
                                            const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb,
                                            lds_f64* frames) {
   constexpr bool REFR = MODE != RT_MODE_REFL, CHAIN = MODE == RT_MODE_CHAIN;
-  constexpr int KLR = MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0;
-  constexpr int KP = rows_pool_slots<MODE, KL_, KP_>();
-  constexpr int KL = rows_lane_frames<MODE, KL_>();
+  constexpr int KLR = PRIM ? 0 : MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0;
+  constexpr int KP = PRIM ? 0 : rows_pool_slots<MODE, KL_, KP_>();
+  constexpr int KL = PRIM ? 0 : rows_lane_frames<MODE, KL_>();
+  if constexpr (PRIM) max_depth = 0;
   const int lane = threadIdx.x & 63;
   const unsigned tile = CAL || !order ? entry : (unsigned)order[entry];
   [[maybe_unused]] uint64_t t_start = 0;
@@ -1554,18 +1561,19 @@ __device__ __forceinline__ void rows_entry(const RtDevScene& S, unsigned entry, 
   if (y >= S.height) return;
   V3 ro, rd;
   camera_ray_px(S, x, y, &ro, &rd);                                         // get_pixel(x as f64, y as f64)
-  const Col c = trace<REFR, NoRec, KL, FC, KLR, CHAIN, KP>(make_ds(S), ro, rd, max_depth, nullptr, frames + lane, frames);
-  store_pixel<F64>(out + (size_t)r * stride, x, c, rgb);
+  const Col c = trace<REFR, NoRec, KL, FC, KLR, CHAIN, KP>(make_ds(S), ro, rd, max_depth, nullptr, PRIM ? nullptr : frames + lane,
+                                                         frames);
+  store_pixel<F64, PRIM>(out + (size_t)r * stride, x, c, rgb);
   if constexpr (CAL)
     if (threadIdx.x == 0) cost[tile] = (uint32_t)(wall_clock64() - t_start);   // vector store
 }
-template <int MODE, bool F64, bool CAL, bool FC, int KL_ = -1, int KP_ = -1>
+template <int MODE, bool F64, bool CAL, bool FC, int KL_ = -1, int KP_ = -1, bool PRIM = false>
 __device__ __forceinline__ void rows_body(const RtDevScene& S, int y_first, int band_rows, int band_pitch, int n_rows,
                                           int max_depth, uint8_t* __restrict__ out, size_t stride,
                                           const int32_t* __restrict__ order, uint32_t* __restrict__ cost, int rgb,
                                           lds_f64* frames) {
-  rows_entry<MODE, F64, CAL, FC, KL_, KP_>(S, blockIdx.x, y_first, band_rows, band_pitch, n_rows, max_depth, out, stride,
-                                           order, cost, rgb, frames);
+  rows_entry<MODE, F64, CAL, FC, KL_, KP_, PRIM>(S, blockIdx.x, y_first, band_rows, band_pitch, n_rows, max_depth, out,
+                                                 stride, order, cost, rgb, frames);
 }
 template <int MODE, int KL_ = -1, int KP_ = -1>
 constexpr int rows_lds_doubles() {

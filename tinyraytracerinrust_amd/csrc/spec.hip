@@ -290,6 +290,10 @@ static std::string spec_kernel(int kind, int mode, bool fc, int f64, int cal) {
 #ifndef RT_SPEC_WAVES_CHAIN
 #define RT_SPEC_WAVES_CHAIN RT_SPEC_WAVES
 #endif
+  // The primary-ray kernel: no frame stack, so its VGPRs (not a fixed budget) set its occupancy.
+#ifndef RT_SPEC_WAVES_PRIM
+#define RT_SPEC_WAVES_PRIM 4
+#endif
   snprintf(waves, sizeof waves, "%d", mode == RT_MODE_CHAIN ? RT_SPEC_WAVES_CHAIN : RT_SPEC_WAVES);
   // stack frames in LDS: 4 waves/SIMD leave 10 KB per one-wave workgroup (the generic kernel's 2
   // frames at 5 waves: 4 KB); RT_SPEC_LDS_FRAMES (diagnostic builds) overrides the mode's default
@@ -303,7 +307,14 @@ static std::string spec_kernel(int kind, int mode, bool fc, int f64, int cal) {
   if (const char* e = getenv("RT_SPEC_KL")) kl = atoi(e);      // diagnostic builds: A/B of the LDS frames
   if (const char* e = getenv("RT_SPEC_KP")) kp = atoi(e);
 #endif
-  if (kind == 0)
+  if (kind == 2)                                              // the primary-ray kernel (rt_device.h PRIM)
+    snprintf(buf, sizeof buf,
+             "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(%d))) "
+             "void rt_spec_prim_%d%d%s {\n"
+             "  rows_body<%d, %s, %s, %s, 0, 0, true>(S, y_first, band_rows, band_pitch, n_rows, 0, out, stride, order, "
+             "cost, rgb, nullptr);\n}\n",
+             RT_SPEC_WAVES_PRIM, f64, cal, args, mode, f64 ? "true" : "false", cal ? "true" : "false", fc ? "true" : "false");
+  else if (kind == 0)
     snprintf(buf, sizeof buf,
              "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(%s))) "
              "void rt_spec_rows_%d%d%s {\n  __shared__ double s_frames[rows_lds_doubles<%d, %d, %d>()];\n"
@@ -323,18 +334,24 @@ static std::string spec_kernel(int kind, int mode, bool fc, int f64, int cal) {
 }
 
 // The kernels a context loads, (kind, f64, cal): kind 0 = the megakernel, 1 = the deferred kernel
-// (reflection-only scenes: their tail-bound launches' choice).  RT_OPT_SPECIALIZE 1: the RGBA8 /
-// RGB8 product launches (f64 = 0, cal = 0); 2: the f64 and calibration instantiations too (tests:
-// every launch of a parity test then runs specialised).  Each kernel is its own program (prelude +
-// one kernel): the programs compile in parallel, and the inliner sees one kernel per module.
+// (reflection-only scenes: their tail-bound launches' choice), 2 = the primary-ray kernel (launches
+// with max_depth 0).  RT_OPT_SPECIALIZE 1: the RGBA8 / RGB8 product launches (f64 = 0, cal = 0); 2: the
+// f64 and calibration instantiations too (tests: every launch of a parity test then runs specialised).
+// Each kernel is its own program (prelude + one kernel): the programs compile in parallel, and the
+// inliner sees one kernel per module.
 struct SpecKernel { int kind, f64, cal; };
 static std::vector<SpecKernel> spec_kernels(const rt_ctx* c) {
   std::vector<SpecKernel> v;
   const int n = c->spec_on >= 2 ? 2 : 1;
-  for (int kind = 0; kind < (c->spec_deferred ? 2 : 1); ++kind)
+  for (int kind = 0; kind < 3; ++kind) {
+    if (kind == 1 && !c->spec_deferred) continue;
     for (int f64 = 0; f64 < n; ++f64)
       for (int cal = 0; cal < n; ++cal) v.push_back({kind, f64, cal});
+  }
   return v;
+}
+static const char* spec_kernel_name(int kind) {
+  return kind == 2 ? "rt_spec_prim_%d%d" : kind == 1 ? "rt_spec_def_%d%d" : "rt_spec_rows_%d%d";
 }
 static std::vector<std::string> spec_programs(const rt_ctx* c) {
   std::vector<std::string> v;
@@ -790,6 +807,7 @@ void spec_drop(rt_ctx* c) {
   c->spec_mod = nullptr;
   memset(c->spec_rows, 0, sizeof c->spec_rows);
   memset(c->spec_def, 0, sizeof c->spec_def);
+  memset(c->spec_prim, 0, sizeof c->spec_prim);
   c->spec_jobs.clear();                                   // drops this context's interest
   c->spec_error.clear();
 }
@@ -830,8 +848,9 @@ int spec_poll(rt_ctx* c) {
     const SpecCode& code = c->spec_jobs[i]->code;
     hipError_t e = hipModuleLoadData(&c->spec_mods[i], code.code.data());
     if (e == hipSuccess) {
-      snprintf(name, sizeof name, k.kind ? "rt_spec_def_%d%d" : "rt_spec_rows_%d%d", k.f64, k.cal);
-      e = hipModuleGetFunction(k.kind ? &c->spec_def[k.f64][k.cal] : &c->spec_rows[k.f64][k.cal], c->spec_mods[i], name);
+      snprintf(name, sizeof name, spec_kernel_name(k.kind), k.f64, k.cal);
+      hipFunction_t* fn = k.kind == 2 ? &c->spec_prim[k.f64][k.cal] : k.kind ? &c->spec_def[k.f64][k.cal] : &c->spec_rows[k.f64][k.cal];
+      e = hipModuleGetFunction(fn, c->spec_mods[i], name);
     }
     if (e != hipSuccess) {
       c->spec_jobs.clear();

@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _is_render(name, kernel):
     """The product row kernel of a dispatch: the generic render_rows_kernel<MODE, F64, CAL, FC> with
-    CAL = false, or the scene-specialised rt_spec_rows_<f64><cal> with cal = 0 (the one calibration
+    CAL = false, or the scene-specialised rt_spec_rows_ / rt_spec_prim_<f64><cal> with cal = 0 (the one calibration
     launch per geometry is excluded)."""
     if kernel != "render_rows_kernel":
         return kernel in name
@@ -29,8 +29,8 @@ def _is_render(name, kernel):
     if m:
         a = [x.strip() for x in m.group(1).split(",")]
         return not (len(a) >= 3 and a[2] == "true")
-    m = re.match(r"rt_spec_rows_(\d)(\d)", name)
-    return bool(m) and m.group(2) == "0"
+    m = re.match(r"rt_spec_(rows|prim)_(\d)(\d)", name)
+    return bool(m) and m.group(3) == "0"
 
 
 def main(tag="r01", config="globes4k", kernel="render_rows_kernel"):
