@@ -957,7 +957,7 @@ typedef LDS_AS double lds_f64;
 // Refraction-chain kernels (RT_MODE_CHAIN): frames of the chain stack kept in LDS.  At 4 waves/SIMD
 // (below) 5 frames fill the 160 KB of a CU (10 KB per one-wave workgroup).
 #ifndef RT_LDS_FRAMES_CHAIN
-#define RT_LDS_FRAMES_CHAIN 1
+#define RT_LDS_FRAMES_CHAIN 0          // round 6: every chain frame in the wave's pool (rows_pool_slots)
 #endif
 // Refraction frames also carry the pending reflection ray (P, D, rp: 7 doubles); the first
 // KLR of them go to LDS after the KL colour frames, [frame][component][lane] likewise.
@@ -981,6 +981,34 @@ typedef LDS_AS double lds_f64;
 constexpr int RT_POOL_HDR = RT_MAX_DEPTH_CAP + RT_MAX_DEPTH_CAP / 2;      // header doubles
 #define LDS_U64 __attribute__((address_space(3))) uint64_t
 #define LDS_U32 __attribute__((address_space(3))) uint32_t
+#define LDS_U8 __attribute__((address_space(3))) uint8_t
+// Pool slots hold (A, hit object) instead of (A, w) (round 6).  Outside the ray-tree mode a frame's
+// weight is a function of the hit object alone: a refraction frame's w is the object's transparency; a
+// reflection frame's is rp = TIR ? refl + (1 - refl) * transp : refl (raytracer.rs:261-265), and a TIR
+// hit refracts only where transp != 0, which in these modes forces refl == +-0, so rp = 0 + 1 * transp
+// = transp exactly; without TIR a reflecting object has transp == 0 (else it would have refracted), so
+// w = refl.  Hence w = (transp != 0 ? transp : refl) of the frame's object (frame_weight), bit for bit,
+// and a slot is 3 doubles + 1 byte: 25 B instead of 32.  Scenes of more than 256 objects keep w.
+#ifndef RT_POOL_OBJ_INDEX
+#define RT_POOL_OBJ_INDEX 1
+#endif
+template <int KP, bool PIDX> constexpr int pool_doubles() { return PIDX ? 3 * KP + (KP + 7) / 8 : 4 * KP; }
+// the weight of a frame whose hit object is o (see RT_POOL_OBJ_INDEX)
+__device__ __forceinline__ double frame_weight(const DS& S, int o) {
+#ifdef RT_SPEC
+  double w = 0.0;
+  spec_for<0, rt_spec::N_OBJECTS>([&](auto I) RT_INL {
+    constexpr int k = decltype(I)::value;
+    RT_REC(O, S, objects, OBJECTS, k);
+    const double t = O->transparency;
+    if (o == k) w = t != 0.0 ? t : O->reflectivity;
+  });
+  return w;
+#else
+  const double t = S.objects[o].transparency;          // per-lane loads (the generic kernels)
+  return t != 0.0 ? t : S.objects[o].reflectivity;
+#endif
+}
 __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {                 // set lanes of m below this one
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -999,10 +1027,13 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
   double fA[RT_MAX_DEPTH_CAP][3];     // parent colour already intensified by (1 - w)
   double fW[RT_MAX_DEPTH_CAP];        // child weight w (transparency or reflectivity)
   constexpr bool POOL = KP > 0 && !(REFR && !CHAIN) && same_type<Rec, NoRec>::value;
+  // pool slots hold the hit object instead of w (RT_POOL_OBJ_INDEX); the scene has <= 256 objects (host)
+  constexpr bool PIDX = POOL && RT_POOL_OBJ_INDEX;
   // frames 0..KL-1 stay in the lanes' own LDS slots (lf); the pool serves frames KL.. (after them at lp)
   LDS_U64* const pool_mask = (LDS_U64*)(lp + KL * 4 * 64);
   LDS_U32* const pool_start = (LDS_U32*)(lp + KL * 4 * 64 + RT_MAX_DEPTH_CAP);
   lds_f64* const pool = lp + KL * 4 * 64 + RT_POOL_HDR;
+  LDS_U8* const pool_obj = (LDS_U8*)(pool + 3 * KP);             // PIDX: [KP] object bytes after [3][KP] doubles
   uint32_t pool_used = 0;             // wave-uniform: slots taken by the pushes so far
   auto put_frame = [&](int f, Col A, double w) {
     if (KL > 0 && f < KL) {
@@ -1015,7 +1046,9 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
     if (POOL && f >= KL) {
       const uint32_t slot = pool_start[f] + lane_rank(pool_mask[f]);
       if (slot < (uint32_t)KP) {
-        *A = {pool[slot], pool[KP + slot], pool[2 * KP + slot]}; *w = pool[3 * KP + slot];
+        *A = {pool[slot], pool[KP + slot], pool[2 * KP + slot]};
+        if constexpr (PIDX) *w = frame_weight(S, pool_obj[slot]);
+        else *w = pool[3 * KP + slot];
         return;
       }
     }
@@ -1026,13 +1059,15 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
     }
   };
   // POOL: the frame every lane still walking pushes in this iteration (they are all at frame f)
-  auto pool_push = [&](bool push, int f, Col A, double w) {
+  auto pool_push = [&](bool push, int f, Col A, double w, int obj) {
     const uint64_t m = __ballot(push);
     const uint32_t start = pool_used;
     if (push) {
       const uint32_t slot = start + lane_rank(m);
       if (slot < (uint32_t)KP) {
-        pool[slot] = A.r; pool[KP + slot] = A.g; pool[2 * KP + slot] = A.b; pool[3 * KP + slot] = w;
+        pool[slot] = A.r; pool[KP + slot] = A.g; pool[2 * KP + slot] = A.b;
+        if constexpr (PIDX) pool_obj[slot] = (uint8_t)obj;
+        else pool[3 * KP + slot] = w;
       } else {
         fA[f][0] = A.r; fA[f][1] = A.g; fA[f][2] = A.b; fW[f] = w;
       }
@@ -1179,7 +1214,7 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
       if (iter < KL) {
         if (pushing) put_frame(iter, push_A, push_w);                     // the lane's own LDS slot
       } else {
-        pool_push(pushing, iter, push_A, push_w);
+        pool_push(pushing, iter, push_A, push_w, oi);
       }
     }
     if (descend) continue;
@@ -1525,8 +1560,13 @@ __device__ __forceinline__ void store_pixel(uint8_t* row, int x, Col c, int rgb)
 #ifndef RT_LDS_POOL_REFL
 #define RT_LDS_POOL_REFL 0
 #endif
+//   round 6, pool slots of 25 B (RT_POOL_OBJ_INDEX), f32 culling (profiles/r09d_anim_pool_sweep.txt; anim120
+//     Mrays/s, MB per 1080p frame): 1 per-lane frame + 122 slots 17 152 / 94.3; 1 + 183: 16 645 / 70.1;
+//     1 + 238: 16 119 / 50.4; 0 + 265 (6.7 KB: 6 waves/SIMD) 16 660 / 61.2; 0 + 320 (8 KB: 5 waves/SIMD)
+//     16 118 / 41.5 (FETCH 7.4 MiB) -- 0 + 320 is kept: the round-5 verdict's traffic bar (<= 48 MB per frame,
+//     FETCH <= 8 MiB at >= 16 000 Mrays/s) at 6 % below the fastest layout.
 #ifndef RT_LDS_POOL_CHAIN
-#define RT_LDS_POOL_CHAIN 122       // + 1 per-lane frame: 6 KB: 26 workgroups per CU, the VGPRs set the occupancy
+#define RT_LDS_POOL_CHAIN 320       // no per-lane frame: 8 KB per one-wave workgroup, 20 per CU (5 waves/SIMD)
 #endif
 template <int MODE, int KL_ = -1, int KP_ = -1>
 constexpr int rows_pool_slots() {
@@ -1578,7 +1618,9 @@ __device__ __forceinline__ void rows_body(const RtDevScene& S, int y_first, int 
 template <int MODE, int KL_ = -1, int KP_ = -1>
 constexpr int rows_lds_doubles() {
   return (rows_lane_frames<MODE, KL_>() * 4 + (MODE == RT_MODE_TREE ? RT_LDS_RFRAMES : 0) * 7) * 64 +
-         (rows_pool_slots<MODE, KL_, KP_>() > 0 ? RT_POOL_HDR + 4 * rows_pool_slots<MODE, KL_, KP_>() : 0);
+         (rows_pool_slots<MODE, KL_, KP_>() > 0
+              ? RT_POOL_HDR + pool_doubles<rows_pool_slots<MODE, KL_, KP_>(), RT_POOL_OBJ_INDEX != 0>()
+              : 0);
 }
 
 // The deferred-shadow kernel's body (reflection-only scenes, or refraction chains on request): one

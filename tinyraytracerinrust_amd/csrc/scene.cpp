@@ -845,6 +845,9 @@ int flatten(const rt_scene& s, FlatScene* out) {
     if (m.texture < 0 && !(nonneg(m.color[0]) && nonneg(m.color[1]) && nonneg(m.color[2]))) f.colour_fast = 0;
     f.objects.push_back(ob);
   }
+  // The chain kernels' pool frames name their hit object in one byte (rt_device.h RT_POOL_OBJ_INDEX):
+  // refraction scenes of more than 256 objects take the ray-tree kernels, which handle chains too.
+  if (f.objects.size() > 256) f.ray_chains = 0;
   if (!f.shadow_early_out) f.shadow_pow = 0;
   // |T| > 1: T^k may overflow to +-inf, and inf * 0 is NaN, so with a zero-transparency object the
   // draw-order product depends on where the zero factor comes (T, T, 0 -> NaN; 0, T, T -> 0): not
