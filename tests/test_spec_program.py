@@ -57,7 +57,7 @@ def test_scene_family_programs():
         assert all("#define RT_SPEC_FAMILY 1" in p for p in progs)
         assert 1 <= len(set(progs)) <= 3, len(set(progs))
         vary = re.search(r"VARY_OBJECTS\[\] = \{([^}]*)\}", progs[0]).group(1).split(",")
-        assert len(vary) == 4 * 224 // 4 and 0 < vary.count("1") < len(vary)
+        assert len(vary) % 4 == 0 and len(vary) // 4 >= 48 and 0 < vary.count("1") < len(vary)   # 4 objects, one mask word per 4 bytes
         # a scene of a structure of its own ("a family of one") keeps its own, exact program -- compiled
         # by the registration (every word a constant: globes.scene's family form spilled 1 392 B/lane)
         g = _scene(scene_text("globes"))

@@ -166,7 +166,10 @@ struct alignas(16) RtObject {
                                     // tighter than blo/bhi (rotated thin rods and slabs); -1: none
   double olo[3], ohi[3];            // that box in obb_leaf's object space, inflated (scene.cpp obb)
   float folo[3], fohi[3];           // olo / ohi as the f32 culling box (RT_CULL32_MARGIN, rounded outward)
-  int32_t pad1[2];
+  int32_t unit_normal;              // 1: the normal is a constant (a plane object): nunit / nunit_len below
+  int32_t pad1;
+  double nunit[3];                  // normalized(get_normal) (raytracer.rs:163), the host's IEEE operations
+  double nunit_len;                 // len(nunit) (vector.rs:57-59's denominator term)
 };
 
 // Order-preserving object hierarchy: a pre-order list of nodes over CONTIGUOUS runs of objects

@@ -166,6 +166,9 @@ struct DS {                         // device view of RtDevScene
 };
 
 constexpr double EPS = RT_EPSILON;
+#ifndef RT_PLANE_SELF_SKIP
+#define RT_PLANE_SELF_SKIP 1        // traversals: a plane distance provably below EPS skips its division
+#endif
 #ifndef RT_PLANE_AXIS
 #define RT_PLANE_AXIS 1             // axis-aligned planes: one product per dot in the traversals
 #endif
@@ -399,6 +402,10 @@ __device__ __forceinline__ int leaf_candidates(cptr<RtLeaf> L, V3 ro, V3 rd, boo
       // t = -num * (1/v_d) is > 0 only if num and v_d have opposite signs (rounding keeps signs;
       // 1/v_d may overflow to +-inf, never to 0).  Otherwise t is <= 0, -0 or NaN: never > EPS.
       if (POS && !((num > 0.0 && v_d < 0.0) || (num < 0.0 && v_d > 0.0))) return 0;
+      // |t| <= |num| / |v_d| (1 + 2^-52)^2 < EPS when |num| <= 2^-22 |v_d| (the product is exact or
+      // rounds towards 0): never accepted.  A ray leaving the plane it starts on (the floor's shadow and
+      // reflection rays) skips the division.
+      if (POS && RT_PLANE_SELF_SKIP && fabs(num) <= 0x1p-22 * fabs(v_d)) return 0;
       double t = -num * (1.0 / v_d);
       if (t >= 0.0) { *t0 = t; return 1; }
     }
@@ -859,14 +866,28 @@ __device__ __forceinline__ V3 refract_dir(V3 i, V3 n, double r, bool* tir) {   /
 // Normal (normalised, :163), material colour at the UV (:165-170), transparency, reflectivity of
 // each lane's hit object -- SCALARISED over the distinct objects hit in this wave (readlane of the
 // first remaining lane), so every object / node / leaf read is wave-uniform (SMEM, no VGPRs).
+// nlen (optional): len(normal) of the normalised normal, the denominator term the Lambert angles and the
+// inside test take (vector.rs:57-59) -- formed once here.  Objects whose normal is a constant (a plane:
+// RtObject::unit_normal) take the host's normalised normal and its length (the same IEEE operations on the
+// same values: bit-identical), so a wave of floor hits skips the normalisation and the length.
+#ifndef RT_UNIT_NORMAL
+#define RT_UNIT_NORMAL 1
+#endif
 __device__ __forceinline__ void shade_inputs(const DS& S, int oi, V3 p, V3* nrm, Col* c, double* transp,
-                                             double* refl) {
+                                             double* refl, double* nlen = nullptr) {
   RT_OPAQUE(p.x);                          // RT_SPEC: keep the per-object work on p in the light loop
   RT_OPAQUE(p.y);                          // (see RT_OPAQUE)
   RT_OPAQUE(p.z);
+  bool unit = false;
   auto shade = [&](cptr<RtObject> O) RT_INL {
-    double u, v;
-    object_normal_uv(S, O, p, O->textured != 0, nrm, &u, &v);
+    double u = 0.0, v = 0.0;                 // a plane's UV is Err -> (0, 0) (math_shapes.rs:196-198)
+    if (RT_UNIT_NORMAL && nlen && O->unit_normal) {
+      *nrm = ld3(O->nunit);
+      *nlen = O->nunit_len;
+      unit = true;
+    } else {
+      object_normal_uv(S, O, p, O->textured != 0, nrm, &u, &v);
+    }
     *c = O->textured ? texture_color(S, O->tex, u, v) : Col{O->color[0], O->color[1], O->color[2]};
     *transp = O->transparency;
     *refl = O->reflectivity;
@@ -891,7 +912,10 @@ __device__ __forceinline__ void shade_inputs(const DS& S, int oi, V3 p, V3* nrm,
     if ((mine >> __lane_id()) & 1) shade(&S.objects[o]);
   }
 #endif
-  *nrm = normalized(*nrm);
+  if (!unit) {
+    *nrm = normalized(*nrm);
+    if (nlen) *nlen = len(*nrm);
+  }
 }
 
 template <class A, class B> struct same_type { static constexpr bool value = false; };
@@ -1120,7 +1144,7 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
     if constexpr (RECORD) slot = rec->begin(depth, ray_type, ro, rd, t_hit, oi, p);
     V3 nrm = {0.0, 0.0, 0.0};
     Col c = {0.0, 0.0, 0.0}, L = {0.0, 0.0, 0.0};
-    double transp = 0.0, refl = 0.0;
+    double transp = 0.0, refl = 0.0, nlen = 0.0;
     if (oi >= 0) {
       // Evaluation order is free (every step is a pure function of the hit), so the shadow
       // rays of a group of lights are traced FIRST, while only the hit point is live, and the
@@ -1140,19 +1164,19 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
         double t;                                                          // :176-197
         t = shadow_transparency<SHARE, OBB>(S, p, sdir, ll);
         if (!have_shading) {
-          shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
+          shade_inputs(S, oi, p, &nrm, &c, &transp, &refl, &nlen);
           L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));                      // ambient (:172)
           have_shading = true;
         }
         if (t == 0.0) continue;                                            // :199-227
-        double ang = rt_acos(dot(sdir, nrm) / (len(sdir) * len(nrm)));
+        double ang = rt_acos(dot(sdir, nrm) / (len(sdir) * nlen));
         if (ang >= PI_D / 2.0) ang = PI_D - ang;
         const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
         const Col lc = intensify<FC>(intensify<FC>(Col{lt->col[0], lt->col[1], lt->col[2]}, inten), t);
         L = cadd<FC>(L, cmul<FC>(c, lc));
       }
       if (!have_shading) {
-        shade_inputs(S, oi, p, &nrm, &c, &transp, &refl);
+        shade_inputs(S, oi, p, &nrm, &c, &transp, &refl, &nlen);
         L = cmul<FC>(c, in_range<FC>(0.6, 0.6, 0.6));
       }
     }
@@ -1165,7 +1189,7 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
       bool inside = false;
       if (depth < max_depth && (refl != 0.0 || (REFR && transp != 0.0))) {
         const V3 nd = scale(rd, -1.0);
-        inside = inside_test(dot(nd, nrm) / (len(nd) * len(nrm)));
+        inside = inside_test(dot(nd, nrm) / (len(nd) * nlen));
       }
       const V3 n2 = inside ? scale(nrm, -1.0) : nrm;
       const double r1 = inside ? 1.45 : 1.0, r2 = inside ? 1.0 : 1.45;

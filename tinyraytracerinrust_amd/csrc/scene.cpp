@@ -571,6 +571,27 @@ static void obb(FlatScene& f, RtObject* ob) {
   }
 }
 
+// ---------------------------------------------------------------- constant normals
+// A plane object's normal is its leaf's constant MathPlane::normal; get_ray_color normalises it
+// (raytracer.rs:163) and every angle divides by its length (vector.rs:57-59).  The kernels' normalized()
+// and len() are IEEE sqrt / division / products in this order (rt_device.h: sqrt_core and recip_core
+// are bit-identical to sqrt and 1.0 / l), so the host forms both once.  Only finite results are kept.
+static void unit_normal(const FlatScene& f, RtObject* ob) {
+  ob->unit_normal = 0;
+  if (ob->node_count != 1 || diag_env("RT_NO_UNIT_NORMAL")) return;
+  const RtLeaf& L = f.leaves[ob->leaf_begin];
+  if (L.kind != RT_N_PLANE) return;
+  const double* a = L.pn[0];
+  const double x = (a[0] * a[0] + a[1] * a[1]) + a[2] * a[2];
+  const double l = sqrt(x), il = 1.0 / l;
+  const double n[3] = {a[0] * il, a[1] * il, a[2] * il};
+  const double nl = sqrt((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]);
+  if (!(std::isfinite(n[0]) && std::isfinite(n[1]) && std::isfinite(n[2]) && std::isfinite(nl) && nl > 0.0)) return;
+  for (int i = 0; i < 3; ++i) ob->nunit[i] = n[i];
+  ob->nunit_len = nl;
+  ob->unit_normal = 1;
+}
+
 // ---------------------------------------------------------------- object hierarchy
 static double box_area(const double* lo, const double* hi) {
   const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
@@ -823,6 +844,7 @@ int flatten(const rt_scene& s, FlatScene* out) {
     }
     ob.leaf_cull = n_leaf_boxes_tighter > 0;
     obb(f, &ob);
+    unit_normal(f, &ob);
     order_literals(f, ob);
     const_filters(f, ob);
     const rt_material& m = o.mat;
