@@ -112,8 +112,12 @@ using rt::fail;
     if (rc_) return rc_;                                                               \
   } while (0)
 
+#ifndef RT_SPEC_MAX_OBJECTS
 #define RT_SPEC_MAX_OBJECTS 32
+#endif
+#ifndef RT_SPEC_MAX_LEAVES
 #define RT_SPEC_MAX_LEAVES 48
+#endif
 #define RT_SPEC_MAX_FAMILIES 16
 
 namespace rt {
