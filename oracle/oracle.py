@@ -80,6 +80,8 @@ def _lib(counting: bool = False):
     lib.orc_num_lights.argtypes = [ctypes.c_void_p]
     lib.orc_camera.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
     lib.orc_light.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    lib.orc_texel_probe.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]
+    lib.orc_texel_probe.restype = ctypes.c_int
     lib.orc_get_pixel.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double,
                                   ctypes.POINTER(ctypes.c_double)]
     lib.orc_render_rows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -170,6 +172,13 @@ class OracleScene:
         out = (ctypes.c_double * 4)()
         self.lib.orc_get_pixel(self.h, float(x), float(y), out)
         return np.array(out[:])
+
+    def texel_probe(self, x: float, y: float):
+        """(object, (x_tex, y_tex, u, v)) of get_pixel(x, y)'s primary hit when its object is textured
+        (texture.rs:27-34's coordinates before truncation), else (-1, None)."""
+        out = (ctypes.c_double * 4)()
+        o = self.lib.orc_texel_probe(self.h, float(x), float(y), out)
+        return (o, tuple(out[:])) if o >= 0 else (-1, None)
 
     def render(self, y0: int = 0, y1: int | None = None, row_step: int = 1, threads: int = 0,
                f64: bool = False, u8: bool = True):

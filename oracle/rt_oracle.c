@@ -1658,6 +1658,30 @@ void orc_get_pixel(const orc_scene *sc, double x, double y, double rgba[4]) {
   rgba[0] = col.r; rgba[1] = col.g; rgba[2] = col.b; rgba[3] = col.a;
 }
 
+/* Texel-boundary probe (tests only): the primary ray of get_pixel(x, y) (camera.rs:58-74), its nearest
+ * hit (raytracer.rs:141-150) and, when the hit object is textured, the texture lookup's coordinates
+ * before truncation (texture.rs:27-34): out = {u * (w - 1), h - v * (h - 1) - 1, u, v}.  Returns the
+ * hit object's index if it is textured, else -1. */
+int orc_texel_probe(const orc_scene *sc, double x, double y, double out[4]) {
+  Ray ray = camera_create_ray(&sc->camera, x, y);
+  NearestCtx nc = {INFINITY, NULL, NULL};
+  for (int i = 0; i < sc->n_objects; ++i) {
+    nc.cur = &sc->objects[i];
+    rtobject_intersects(&sc->objects[i], ray, add_nearest, &nc);
+  }
+  const RTObject *obj = nc.nearest_obj;
+  if (!obj || !obj->material.textured) return -1;
+  Vec point = v_add(ray.point, v_scale(ray.direction, nc.nearest));
+  UV uv = {0.0, 0.0};
+  if (!shape_get_uv(obj->shape, point, &uv)) { uv.u = 0.0; uv.v = 0.0; }
+  const Texture *t = obj->material.texture;
+  out[0] = uv.u * (double)(t->w - 1);
+  out[1] = (double)t->h - (uv.v * (double)(t->h - 1)) - 1.0;
+  out[2] = uv.u;
+  out[3] = uv.v;
+  return (int)(obj - sc->objects);
+}
+
 typedef struct {
   const orc_scene *sc;
   int y0, y1, tid, nthreads, row_step;

@@ -318,16 +318,49 @@ RT_FN V3 leaf_normal(cptr<RtLeaf> L, V3 p, bool fin) {
   return {1.0, 1.0, 1.0};
 }
 
-// MathSphere::get_uv_coordinates (:82-114): the centre is subtracted BEFORE the inverse transform
-RT_FN void sphere_uv(cptr<RtLeaf> L, V3 p, double* u, double* v) {
+// MathSphere::get_uv_coordinates (:82-114): the centre is subtracted BEFORE the inverse transform.
+// tw, th > 0 (a textured object's texture size): the texel-boundary guard.  The texture lookup truncates
+// x = u (tw - 1) and y = th - v (th - 1) - 1 (texture.rs:27-34), and u, v come from two acos and a sin that
+// may differ from glibc's (the reference's libm) by an ulp (rt_acos, ocml's sin).  From those ulps the
+// guard bounds how far the lane's x and y can be from glibc's (through sin's slope at phi, acos's slope
+// 1 / sqrt(1 - r^2) at r, and every rounding on the way, times 16); a lane whose x or y lies within that
+// bound of an integer (or of a clamp edge, or whose r is near +-1 or not finite) evaluates phi, sin(phi)
+// and theta again with the correctly rounded rt_acos_cr / rt_sin_cr (rt_math.h) -- glibc's values except
+// where glibc itself is not correctly rounded.  Far from a boundary both sides truncate to the same texel,
+// and the guard costs ~30 flops per textured hit; a 4K frame has ~1e-12 of its hits near a boundary.
+#ifndef RT_TEXEL_SAFE
+#define RT_TEXEL_SAFE 1
+#endif
+__device__ __forceinline__ double ulp_bound(double a) { return fabs(a) * 0x1p-52 + 0x1p-1074; }
+__device__ __forceinline__ bool near_int(double a, double m) { return !(fabs(a - rint(a)) > m); }   // NaN: near
+RT_FN void sphere_uv(cptr<RtLeaf> L, V3 p, double* u, double* v, int tw = 0, int th = 0) {
   V3 q = xf(L->inv, sub(p, ld3(L->c)));           // per shaded hit only: no short form
   q = scale(normalized(q), 1.0 - EPS);
-  double phi = rt_acos(-((0.0 * q.x + 1.0 * q.y) + 0.0 * q.z));             // up = (0,1,0)
+  const double cy = -((0.0 * q.x + 1.0 * q.y) + 0.0 * q.z);                  // up = (0,1,0)
+  const double cz = (q.x * 0.0 + q.y * 0.0) + q.z * -1.0;                    // u_zero = (0,0,-1)
+  const bool flip = (-1.0 * q.x + 0.0 * q.y) + 0.0 * q.z > 0.0;              // u_qrtr = (-1,0,0)
+  double phi = rt_acos(cy);
   if (isnan(phi)) phi = 0.0;
-  double theta = (rt_acos(((q.x * 0.0 + q.y * 0.0) + q.z * -1.0) / sin(phi))) / (2.0 * PI_D);   // u_zero = (0,0,-1)
+  const double sp = sin(phi), r = cz / sp, ac = rt_acos(r);
+  double theta = ac / (2.0 * PI_D);
   if (isnan(theta)) theta = 0.0;
   *v = phi / PI_D;
-  *u = ((-1.0 * q.x + 0.0 * q.y) + 0.0 * q.z > 0.0) ? 1.0 - theta : theta;  // u_qrtr = (-1,0,0)
+  *u = flip ? 1.0 - theta : theta;
+  if (RT_TEXEL_SAFE && tw > 0) {
+    const double x = *u * (double)(tw - 1), y = (double)th - (*v * (double)(th - 1)) - 1.0;
+    const double ey = (double)(th - 1) * (2.0 * ulp_bound(phi) / PI_D + ulp_bound(*v)) + 2.0 * ulp_bound(y);
+    const double er = 0x1p-50 + 4.0 * ulp_bound(phi) / fabs(sp);
+    const double ea = fabs(r) * er / sqrt(fmax(1.0 - r * r, 0x1p-60)) + 2.0 * ulp_bound(ac);
+    const double ex = (double)(tw - 1) * (ea / (2.0 * PI_D) + 2.0 * ulp_bound(*u)) + 2.0 * ulp_bound(x);
+    if (!(fabs(r) < 1.0 - 0x1p-26) || near_int(x, 16.0 * ex) || near_int(y, 16.0 * ey)) {
+      phi = rt_acos_cr(cy);                                                  // the rare lanes: rt_math.h
+      if (isnan(phi)) phi = 0.0;
+      theta = rt_acos_cr(cz / rt_sin_cr(phi)) / (2.0 * PI_D);
+      if (isnan(theta)) theta = 0.0;
+      *v = phi / PI_D;
+      *u = flip ? 1.0 - theta : theta;
+    }
+  }
 }
 
 // Candidate hit distances of one primitive for the world ray (ro, rd):
@@ -777,10 +810,12 @@ RT_FN void object_normal_uv(const DS& S, cptr<RtObject> O, V3 p, bool want_uv, V
   const bool fin = wave_finite(p);
   *u = 0.0;
   *v = 0.0;
+  // want_uv: the object is textured; its texture's size arms sphere_uv's texel-boundary guard
+  const int tw = want_uv ? S.textures[O->tex].w : 0, th = want_uv ? S.textures[O->tex].h : 0;
   if (cnt == 1) {
     RT_REC(L, S, leaves, LEAVES, N[0].leaf);
     *n = leaf_normal(L, p, fin);
-    if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
+    if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v, tw, th);
     return;
   }
   uint32_t in = 0, on = 0;
@@ -823,7 +858,7 @@ RT_FN void object_normal_uv(const DS& S, cptr<RtObject> O, V3 p, bool want_uv, V
     if (!((__ballot(sel == l) >> lane) & 1)) continue;
     RT_REC(L, S, leaves, LEAVES, l);
     *n = leaf_normal(L, p, fin);
-    if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v);
+    if (want_uv && L->kind == RT_N_SPHERE) sphere_uv(L, p, u, v, tw, th);
   }
   if (neg) *n = scale(*n, -1.0);
 }
@@ -849,6 +884,31 @@ RT_FN Col texture_color(const DS& S, int tex, double u, double v) {
 // the acos itself.
 __device__ __forceinline__ bool inside_test(double cin) {
   return cin < -1e-15 ? cin >= -1.0 : (cin > 1e-15 ? false : rt_acos(cin) >= PI_D / 2.0);
+}
+// inside_test's "outside" answer without the square root and the division, for cin = d / (len(a) * nl)
+// with q = dot(a, a) (len(a) = sqrt(q)): when d > 0 and d^2 > 1e-30 q nl^2 (1 + 2^-40), with the right
+// side a normal double, the computed cin exceeds 1e-15 -- sqrt, product and quotient round by 2^-53
+// each, the squares and products here by as much, and 2^-40 covers them all -- so inside_test answers
+// false.  Anything else (NaN, overflow, grazing, inside) takes the exact path.  A wave of hits seen
+// from outside (floor pixels, every primary hit) skips len() and the division.
+#ifndef RT_INSIDE_FAST
+#define RT_INSIDE_FAST 1
+#endif
+__device__ __forceinline__ bool outside_certain(double d, double q, double nl) {
+  const double rhs = (1e-30 * q) * (nl * nl) * (1.0 + 0x1p-40);
+  return d > 0.0 && rhs >= 0x1p-1000 && d * d > rhs;
+}
+
+// ang / (PI / 2) of the Lambert term (raytracer.rs:216-218) for ang in [0, PI/2): an acos result there is
+// +0 or at least acos(1 - 2^-53) > 1e-8 (never subnormal), so div_core's conditions hold (no scaling in
+// either v_div_scale; a zero numerator keeps its sign through v_div_fixup): the compiler's division
+// minus its identities, bit-identical.
+__device__ __forceinline__ double lambert_ratio(double ang) {
+#if RT_FAST_SQRT
+  return div_core(ang, PI_D / 2.0);
+#else
+  return ang / (PI_D / 2.0);
+#endif
 }
 
 __device__ __forceinline__ V3 reflect_dir(V3 i, V3 n) {                    // raytracer.rs:332-334
@@ -1171,7 +1231,7 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
         if (t == 0.0) continue;                                            // :199-227
         double ang = rt_acos(dot(sdir, nrm) / (len(sdir) * nlen));
         if (ang >= PI_D / 2.0) ang = PI_D - ang;
-        const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - (ang / (PI_D / 2.0)) : 0.0;
+        const double inten = (ang < (PI_D / 2.0) && ang >= 0.0) ? 1.0 - lambert_ratio(ang) : 0.0;
         const Col lc = intensify<FC>(intensify<FC>(Col{lt->col[0], lt->col[1], lt->col[2]}, inten), t);
         L = cadd<FC>(L, cmul<FC>(c, lc));
       }
@@ -1189,7 +1249,9 @@ RT_FN Col trace(const DS& S, V3 ro, V3 rd, int max_depth, Rec* rec = nullptr, ld
       bool inside = false;
       if (depth < max_depth && (refl != 0.0 || (REFR && transp != 0.0))) {
         const V3 nd = scale(rd, -1.0);
-        inside = inside_test(dot(nd, nrm) / (len(nd) * nlen));
+        const double d = dot(nd, nrm);
+        if (!(RT_INSIDE_FAST && outside_certain(d, dot(nd, nd), nlen)))
+          inside = inside_test(d / (len(nd) * nlen));
       }
       const V3 n2 = inside ? scale(nrm, -1.0) : nrm;
       const double r1 = inside ? 1.45 : 1.0, r2 = inside ? 1.0 : 1.45;

@@ -68,3 +68,101 @@ RT_HD static inline double rt_acos(double x) {
   const double e = (pi_hi - a) - h;
   return a + ((e + pi_lo) - 2.0 * (sl + s * r));
 }
+
+// ---------------------------------------------------------------- correctly rounded acos / sin
+// For the sphere UV's texel-boundary path only (rt_device.h sphere_texel_uv): a texel coordinate within
+// rounding of an integer decides the texel by the last bit of acos / sin, where rt_acos and ocml's sin may
+// differ from glibc's by an ulp.  These evaluate in double-double (error-free transforms on FMA, Taylor
+// coefficients as double-double constants) to ~2^-100 relative and round once, so they return the
+// correctly rounded result except for values within ~2^-100 of a rounding midpoint; glibc 2.35's acos /
+// sin are themselves correctly rounded on all but ~0.05 % / ~0.14 % of inputs (measured against
+// libquadmath, tests/test_rt_math.py).  Slow (hundreds of flops) and only ever taken by the rare lanes
+// that need them.
+struct rt_dd { double hi, lo; };
+RT_HD static inline rt_dd rt_two_sum(double a, double b) {
+  const double s = a + b, bb = s - a;
+  return {s, (a - (s - bb)) + (b - bb)};
+}
+RT_HD static inline rt_dd rt_fast_two_sum(double a, double b) {      // |a| >= |b| (or a == 0)
+  const double s = a + b;
+  return {s, b - (s - a)};
+}
+RT_HD static inline rt_dd rt_dd_add(rt_dd a, rt_dd b) {
+  rt_dd s = rt_two_sum(a.hi, b.hi);
+  const rt_dd t = rt_two_sum(a.lo, b.lo);
+  s.lo += t.hi;
+  s = rt_fast_two_sum(s.hi, s.lo);
+  s.lo += t.lo;
+  return rt_fast_two_sum(s.hi, s.lo);
+}
+RT_HD static inline rt_dd rt_dd_mul(rt_dd a, rt_dd b) {
+  const double p = a.hi * b.hi;
+  double e = fma(a.hi, b.hi, -p);
+  e += a.hi * b.lo + a.lo * b.hi;
+  return rt_fast_two_sum(p, e);
+}
+// sin(t) and cos(t) for a double-double |t| <= pi/4: Taylor to t^23 / t^24 (next terms < 2^-92 relative)
+RT_HD static inline rt_dd rt_sin_poly_dd(rt_dd t) {
+  const double c[11][2] = {
+      {-0x1.5555555555555p-3, -0x1.5555555555555p-57}, {0x1.1111111111111p-7, 0x1.1111111111111p-63},
+      {-0x1.a01a01a01a01ap-13, -0x1.a01a01a01a01ap-73}, {0x1.71de3a556c734p-19, -0x1.c154f8ddc6c00p-73},
+      {-0x1.ae64567f544e4p-26, 0x1.c062e06d1f209p-80}, {0x1.6124613a86d09p-33, 0x1.f28e0cc748ebep-87},
+      {-0x1.ae7f3e733b81fp-41, -0x1.1d8656b0ee8cbp-97}, {0x1.952c77030ad4ap-49, 0x1.ac981465ddc6cp-103},
+      {-0x1.2f49b46814157p-57, -0x1.2650f61dbdcb4p-112}, {0x1.71b8ef6dcf572p-66, -0x1.d043ae40c4647p-120},
+      {-0x1.761b41316381ap-75, 0x1.3423c7d91404fp-130}};            // (-1)^k / (2k+1)!, k = 1..11
+  const rt_dd u = rt_dd_mul(t, t);
+  rt_dd acc = {c[10][0], c[10][1]};
+#pragma unroll
+  for (int k = 9; k >= 0; --k) acc = rt_dd_add(rt_dd_mul(acc, u), rt_dd{c[k][0], c[k][1]});
+  return rt_dd_add(t, rt_dd_mul(t, rt_dd_mul(u, acc)));
+}
+RT_HD static inline rt_dd rt_cos_poly_dd(rt_dd t) {
+  const double c[12][2] = {
+      {-0x1.0000000000000p-1, 0.0}, {0x1.5555555555555p-5, 0x1.5555555555555p-59},
+      {-0x1.6c16c16c16c17p-10, 0x1.f49f49f49f49fp-65}, {0x1.a01a01a01a01ap-16, 0x1.a01a01a01a01ap-76},
+      {-0x1.27e4fb7789f5cp-22, -0x1.cbbc05b4fa99ap-76}, {0x1.1eed8eff8d898p-29, -0x1.2aec959e14c06p-83},
+      {-0x1.93974a8c07c9dp-37, -0x1.05d6f8a2efd1fp-92}, {0x1.ae7f3e733b81fp-45, 0x1.1d8656b0ee8cbp-101},
+      {-0x1.6827863b97d97p-53, -0x1.eec01221a8b0bp-107}, {0x1.e542ba4020225p-62, 0x1.ea72b4afe3c2fp-120},
+      {-0x1.0ce396db7f853p-70, 0x1.aebcdbd20331cp-124}, {0x1.f2cf01972f578p-80, -0x1.9ada5fcc1ab14p-135}};   // (-1)^k / (2k)!
+  const rt_dd u = rt_dd_mul(t, t);
+  rt_dd acc = {c[11][0], c[11][1]};
+#pragma unroll
+  for (int k = 10; k >= 0; --k) acc = rt_dd_add(rt_dd_mul(acc, u), rt_dd{c[k][0], c[k][1]});
+  return rt_dd_add(rt_dd{1.0, 0.0}, rt_dd_mul(u, acc));
+}
+// asin(t) for a double-double |t| <= 1/2: fdlibm's asin (about an ulp) as the start, one Newton step on
+// sin in double-double (the start's error squared is ~2^-106; the correction itself needs only double).
+RT_HD static inline rt_dd rt_asin_dd(rt_dd t) {
+  const double a0 = t.hi + t.hi * rt_asin_r(t.hi * t.hi);
+  const rt_dd f = rt_dd_add(rt_sin_poly_dd(rt_dd{a0, 0.0}), rt_dd{-t.hi, -t.lo});     // sin(a0) - t
+  return rt_fast_two_sum(a0, -f.hi / cos(a0));
+}
+RT_HD static inline double rt_acos_cr(double x) {
+  const rt_dd pi = {0x1.921fb54442d18p+1, 0x1.1a62633145c07p-53}, pio2 = {0x1.921fb54442d18p+0, 0x1.1a62633145c07p-54};
+  const double ax = fabs(x);
+  if (!(ax < 1.0)) return rt_acos(x);                  // +-1 (exact), |x| > 1 and NaN (NaN)
+  if (ax <= 0.5) {                                     // pi/2 - asin(x)
+    const rt_dd r = rt_dd_add(pio2, rt_asin_dd(rt_dd{-x, 0.0}));
+    return r.hi + r.lo;
+  }
+  const double z = (1.0 - ax) * 0.5;                   // exact (Sterbenz)
+  const double s = sqrt(z);
+  const rt_dd sd = rt_fast_two_sum(s, fma(-s, s, z) / (s + s));     // sqrt(z) to ~2^-106
+  const rt_dd a = rt_asin_dd(sd);
+  const rt_dd a2 = {2.0 * a.hi, 2.0 * a.lo};            // 2 asin(sqrt z), exact scaling
+  if (x > 0.0) return a2.hi + a2.lo;
+  const rt_dd r = rt_dd_add(pi, rt_dd{-a2.hi, -a2.lo}); // pi - 2 asin(sqrt z)
+  return r.hi + r.lo;
+}
+// sin(x) for x in [0, pi] (the sphere UV's phi = acos(...)); other x: the platform's sin.  pi/2 - x and
+// pi - x are exact (Sterbenz) on their branches; pi is carried as a double-double.
+RT_HD static inline double rt_sin_cr(double x) {
+  const double pio2_hi = 0x1.921fb54442d18p+0, pio2_lo = 0x1.1a62633145c07p-54;
+  const double pi_hi = 0x1.921fb54442d18p+1, pi_lo = 0x1.1a62633145c07p-53;
+  if (!(x >= 0.0 && x <= pi_hi)) return sin(x);
+  rt_dd r;
+  if (x <= 0x1.921fb54442d18p-1) r = rt_sin_poly_dd(rt_dd{x, 0.0});                          // x <= pi/4
+  else if (x <= 0x1.2d97c7f3321d2p+1) r = rt_cos_poly_dd(rt_fast_two_sum(pio2_hi - x, pio2_lo));   // <= 3pi/4
+  else r = rt_sin_poly_dd(rt_fast_two_sum(pi_hi - x, pi_lo));
+  return r.hi + r.lo;
+}
