@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=0)
     ap.add_argument("--generic", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="ablation libraries: do not require equal frames")
     ap.add_argument("--levels", default="", help="per library (in order): its RT_OPT_SPECIALIZE level, e.g. 1,2 "
                                                    "(a library path may repeat); default 1 (0 with --generic)")
     a = ap.parse_args()
@@ -75,7 +76,7 @@ def main():
             torch.cuda.synchronize()
             res[i].append(e0.elapsed_time(e1) / n)
     for i in range(1, len(outs)):
-        if not torch.equal(outs[i], outs[0]):
+        if not a.no_check and not torch.equal(outs[i], outs[0]):
             raise SystemExit(f"{a.libs[i]}: frame differs from {a.libs[0]}'s")
     print(f"{a.config} ({'generic' if a.generic else 'specialised'}), {n} frames per measurement, ms per frame, median of {a.rounds}:")
     for path, level, v in zip(a.libs, levels, res):
