@@ -394,7 +394,8 @@ static_assert(RT_WFP_COUNT + 5 <= 64, "wavefront counter block: 256 bytes");
 
 // The object's nearest accepted distance for one ray: nearest_hit's body for one object, its best
 // starting at +inf (the leaf boxes' tmax only shrinks, as share_prev requires).
-__device__ __forceinline__ double wfp_object_nearest(const DS& S, int o, V3 ro, V3 rd, const CullRay& cr) {
+__device__ __forceinline__ double wfp_object_nearest(const DS& S, int o, V3 ro, V3 rd, const CullR& cr) {
+  const bool cf_ok = RT_CONST_FILTER && const_filter_range(ro, rd);
   cptr<RtObject> O = &S.objects[o];
   const bool fin = wave_finite(ro, rd);
   double best = INFINITY;
@@ -404,11 +405,11 @@ __device__ __forceinline__ double wfp_object_nearest(const DS& S, int o, V3 ro, 
     cptr<RtLeaf> L = &S.leaves[l];
     if (O->leaf_cull) {
       if (L->cull == RT_CULL_ALWAYS) continue;
-      if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, cull_tmax(best))) continue;
+      if (L->cull == RT_CULL_BOX && !RT_BOX_MAY_HIT(L, blo, bhi, cr, RT_CULL_TMAX(best))) continue;
     }
     double t0 = 0.0, t1 = 0.0;
     const int n = leaf_candidates<true>(L, ro, rd, fin, &t0, &t1, RT_SPHERE_SHARE ? &shr : nullptr);
-    const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && L->filter_const && !isnan(cr.inv.x));
+    const bool filtered = L->prog_end != L->prog_begin && !(cf_ok && L->filter_const);
     if (n >= 1 && t0 > EPS && t0 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t0))))) best = t0;
     if (n >= 2 && t1 > EPS && t1 < best && (!filtered || leaf_filter(S, L, add(ro, scale(rd, t1))))) best = t1;
   }
@@ -417,10 +418,11 @@ __device__ __forceinline__ double wfp_object_nearest(const DS& S, int o, V3 ro, 
 
 // Filtered hits of the object with EPS < t < dist on one shadow ray (shadow_transparency's body for
 // one object); a zero-transparency object stops at its first.
-__device__ __forceinline__ uint32_t wfp_object_shadow(const DS& S, int o, V3 p, V3 dir, double dist, const CullRay& cr) {
+__device__ __forceinline__ uint32_t wfp_object_shadow(const DS& S, int o, V3 p, V3 dir, double dist, const CullR& cr) {
   cptr<RtObject> O = &S.objects[o];
   const bool fin = wave_finite(p, dir);
-  const double tmax = cull_tmax(dist);
+  const bool cf_ok = RT_CONST_FILTER && const_filter_range(p, dir);
+  const CullT tmax = RT_CULL_TMAX(dist);
   const bool zero = O->transparency == 0.0;
   uint32_t cnt = 0;
   SphereShare shr = {0.0, 0.0, 0.0};
@@ -429,11 +431,11 @@ __device__ __forceinline__ uint32_t wfp_object_shadow(const DS& S, int o, V3 p, 
     cptr<RtLeaf> L = &S.leaves[l];
     if (O->leaf_cull) {
       if (L->cull == RT_CULL_ALWAYS) continue;
-      if (L->cull == RT_CULL_BOX && !box_may_hit(L->blo, L->bhi, cr, tmax)) continue;
+      if (L->cull == RT_CULL_BOX && !RT_BOX_MAY_HIT(L, blo, bhi, cr, tmax)) continue;
     }
     double t0 = 0.0, t1 = 0.0;
     const int n = leaf_candidates<true>(L, p, dir, fin, &t0, &t1, RT_SPHERE_SHARE ? &shr : nullptr);
-    const bool filtered = L->prog_end != L->prog_begin && !(RT_CONST_FILTER && L->filter_const && !isnan(cr.inv.x));
+    const bool filtered = L->prog_end != L->prog_begin && !(cf_ok && L->filter_const);
     if (n >= 1 && t0 > EPS && t0 < dist && (!filtered || leaf_filter(S, L, add(p, scale(dir, t0))))) {
       ++cnt;
       if (zero) return cnt;
@@ -463,7 +465,7 @@ __device__ __forceinline__ bool wf_get_ray(const RtDevScene& S, const WfLevel& l
 // One wave per 64 rays of level d (in key order).  SHADOW = false: every object whose box the ray
 // meets; true: per light, every object whose box the shadow segment meets (objects of transparency 1
 // skipped, as shadow_transparency does).
-// Each lane walks its own path through the hierarchy (one 64-byte RtTrav record per step, which
+// Each lane walks its own path through the hierarchy (one 32-byte RtTravC record per step, which
 // carries the object's box and flags): a wave-uniform walk visits the union of its 64 rays' paths,
 // measured 4-20 % slower here (profiles/r03m_pairs_fractal_timing.txt).
 // A step's record load is the walk's latency: one dependent per-lane load per node, ~100 of them
@@ -477,7 +479,7 @@ __device__ __forceinline__ bool wf_get_ray(const RtDevScene& S, const WfLevel& l
 #define RT_WFP_CAND_WAVES_N 4
 #endif
 constexpr int RT_WFP_CAND_WAVES = RT_WFP_CAND_WAVES_N;
-constexpr uint32_t RT_WFP_LDS_TRAV_MAX = 640;     // nodes (40 KB) staged at most; larger: global loads
+constexpr uint32_t RT_WFP_LDS_TRAV_MAX = 1280;    // nodes (40 KB of RtTravC) staged at most; larger: global loads
 #ifndef RT_WFP_MAX_RANGES_LOG2
 #define RT_WFP_MAX_RANGES_LOG2 2                     // at most 4 hierarchy ranges per ray (below)
 #endif
@@ -506,7 +508,7 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
   extern __shared__ __attribute__((aligned(16))) uint8_t s_trav[];
   // hcnt != nullptr: the pairs' histogram by object for the bucket sort (its histogram launch skipped),
   // counted in LDS (after the staged hierarchy) and added to hcnt once per workgroup
-  uint32_t* const s_hist = (uint32_t*)(s_trav + (LDS_TRAV ? (size_t)S.n_trav * sizeof(RtTrav) : 0));
+  uint32_t* const s_hist = (uint32_t*)(s_trav + (LDS_TRAV ? (size_t)S.n_trav * sizeof(RtTravC) : 0));
   const int lane = threadIdx.x & 63, wv = (int)(threadIdx.x >> 6);
   uint32_t* sk = sk_all[LDS_TRAV ? wv : 0];
   uint32_t* sv = sv_all[LDS_TRAV ? wv : 0];
@@ -528,9 +530,9 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
   if (hcnt)
     for (uint32_t b = threadIdx.x; b < (uint32_t)S.n_objects; b += blockDim.x) s_hist[b] = 0;
   if constexpr (LDS_TRAV) {                                   // the hierarchy into LDS, once per workgroup
-    const uint4* g = (const uint4*)S.trav;
+    const uint4* g = (const uint4*)S.trav_c;
     uint4* l = (uint4*)s_trav;
-    for (uint32_t q = threadIdx.x; q < (uint32_t)S.n_trav * (sizeof(RtTrav) / 16); q += blockDim.x) l[q] = g[q];
+    for (uint32_t q = threadIdx.x; q < (uint32_t)S.n_trav * (sizeof(RtTravC) / 16); q += blockDim.x) l[q] = g[q];
   }
   if (LDS_TRAV || hcnt) __syncthreads();
   const WfLevel lv = wf_level(A, d);
@@ -578,21 +580,23 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
     nb += c;
   };
   auto walk = [&](bool act0, V3 o, V3 dir, double tmax, uint32_t id, int t0, int nt) {   // nodes [t0, nt)
-    const CullRay cr = cull_ray(o, dir);
-    const RtTrav* __restrict__ TR = LDS_TRAV ? (const RtTrav*)(const void*)s_trav : S.trav;
+    const CullRayF cr = cull_ray_f(o, dir);
+    const float tm = (float)tmax;
+    const RtTravC* __restrict__ TR = LDS_TRAV ? (const RtTravC*)(const void*)s_trav : S.trav_c;
     int t = act0 ? t0 : nt;
     while (__ballot(t < nt)) {
       bool h = false;
       int ob = 0;
       if (t < nt) {
-        const RtTrav T = TR[t];
-        const bool in = box_may_hit(T.blo, T.bhi, cr, tmax);
+        const RtTravC T = TR[t];
+        const bool in = fbox_may_hit(T.lo, T.hi, cr, tm);
+        const int cull = (int)((T.skip_flags >> 28) & 3u);
         if (T.obj < 0) {
-          t = in ? t + 1 : T.skip;
+          t = in ? t + 1 : (int)(T.skip_flags & 0x0fffffffu);
         } else {
           ++t;
           ob = T.obj;
-          h = T.cull != RT_CULL_ALWAYS && !(SHADOW && T.shadow_skip) && (T.cull != RT_CULL_BOX || in);
+          h = cull != RT_CULL_ALWAYS && !(SHADOW && (T.skip_flags >> 30)) && (cull != RT_CULL_BOX || in);
         }
       }
       emit(h, (uint32_t)ob, id);
@@ -618,7 +622,7 @@ __global__ __launch_bounds__(64 * RT_WFP_CAND_WAVES) void wfp_cand_kernel(RtDevS
       double bound = INFINITY;
       if (d > 0) {
         const int32_t par = live ? lv.par[j] : -1;
-        const CullRay cr = cull_ray(ro, rd);
+        const CullR cr = RT_CULL_RAY(ro, rd);
         uint64_t todo = __ballot(live && par >= 0);
         while (todo) {                     // the children of one shading wave: mostly one parent
           const int pu = __builtin_amdgcn_readlane(par, (int)__builtin_ctzll(todo));
@@ -679,7 +683,7 @@ __global__ __launch_bounds__(64) void wfp_near_eval_kernel(RtDevScene S, WfArena
       j = P.val_s[i];
       live = wf_get_ray(S, lv, d, j, y_first, band_rows, band_pitch, n_rows, &ro, &rd);
     }
-    const CullRay cr = cull_ray(ro, rd);
+    const CullR cr = RT_CULL_RAY(ro, rd);
     double best = INFINITY;
     uint64_t todo = __ballot(live);
     while (todo) {
@@ -750,7 +754,7 @@ __global__ __launch_bounds__(64) void wfp_shadow_eval_kernel(RtDevScene S, WfPai
       len_inv(l, &ll, &ill);
       sdir = scale(l, ill);
     }
-    const CullRay cr = cull_ray(p, sdir);
+    const CullR cr = RT_CULL_RAY(p, sdir);
     uint32_t cnt = 0;
     uint64_t todo = __ballot(live);
     while (todo) {
@@ -941,7 +945,7 @@ static int wfp_level(rt_ctx* c, hipStream_t st, const WfArena& A, size_t R, int 
       // as many workgroups as the CUs hold at once (the LDS-staged hierarchy sets it); they take the
       // level's rays grid-stride and stage the hierarchy once each (round 5's first form launched
       // 16 per CU: on the small levels most of them only staged and found no ray)
-      const size_t lds = (size_t)c->dev.n_trav * sizeof(RtTrav) + hist_lds;
+      const size_t lds = (size_t)c->dev.n_trav * sizeof(RtTravC) + hist_lds;
       int& occ = c->wfp_occ[shadow ? 1 : 0];                    // queried once per context and LDS size
       if (occ < 1 || c->wfp_occ_lds[shadow ? 1 : 0] != lds) {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)(shadow ? wfp_cand_kernel<true, true> : wfp_cand_kernel<false, true>),

@@ -186,6 +186,17 @@ struct alignas(16) RtTrav {
   int32_t pad0[2];
 };
 
+// A hierarchy node in the form the generic kernels' walks read (rt_device.h walk_trav: one node per step,
+// a dependent scalar load; the wavefront path's per-lane walk, staged in LDS): 32 B instead of RtTrav's
+// 96 -- the f32 culling box and the node words, cull and shadow_skip packed above the 28-bit skip -- two
+// nodes per 64-byte scalar-cache line.  (RtTrav's f32 box sits past its first line: fractal.scene's
+// 300-node walks read two lines per step and its wavefront level-0 trace ran 2.9x longer.)
+struct alignas(16) RtTravC {
+  float lo[3], hi[3];               // RtTrav::fblo / fbhi
+  int32_t obj;                      // RtTrav::obj
+  uint32_t skip_flags;              // skip | cull << 28 | shadow_skip << 30
+};
+
 struct RtTexture {
   int64_t offset;                   // byte offset of RGBA8 data in the texel pool
   int32_t w, h;
@@ -203,6 +214,8 @@ struct RtDevScene {
   const RtObject* objects;
   const RtTrav* trav;
   const RtTrav* strav;              // shadow rays of scenes without a transparent object (any order is exact)
+  const RtTravC* trav_c;            // trav and strav, compact (the generic kernels' walks, the wavefront walk)
+  const RtTravC* strav_c;
   const RtNode* nodes;
   const RtLeaf* leaves;
   const RtProg* prog;

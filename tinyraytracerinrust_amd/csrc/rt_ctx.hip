@@ -139,6 +139,19 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   std::vector<uint8_t> blob;
   size_t o_obj = put(blob, f.objects), o_trav = put(blob, f.trav), o_strav = put(blob, f.strav), o_nodes = put(blob, f.nodes),
          o_leaves = put(blob, f.leaves);
+  std::vector<RtTravC> travc, stravc;
+  for (const auto* src : {&f.trav, &f.strav}) {
+    std::vector<RtTravC>& dst = src == &f.trav ? travc : stravc;
+    dst.resize(src->size());
+    for (size_t i = 0; i < src->size(); ++i) {
+      const RtTrav& t = (*src)[i];
+      if ((uint32_t)t.skip >= (1u << 28)) return fail(RT_ERR_UNSUPPORTED, "object hierarchy of more than 2^28 nodes");
+      for (int k = 0; k < 3; ++k) { dst[i].lo[k] = t.fblo[k]; dst[i].hi[k] = t.fbhi[k]; }
+      dst[i].obj = t.obj;
+      dst[i].skip_flags = (uint32_t)t.skip | (uint32_t)t.cull << 28 | (uint32_t)(t.shadow_skip ? 1 : 0) << 30;
+    }
+  }
+  const size_t o_travc = put(blob, travc), o_stravc = put(blob, stravc);
   size_t o_prog = put(blob, f.prog), o_lights = put(blob, f.lights), o_tex = put(blob, f.textures);
   size_t o_texels = put(blob, f.texels);
   // camera_ray's terms of the integer pixels (rt_device.h camera_ray_px): the same expressions in the
@@ -161,6 +174,8 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
   d.trav = (const RtTrav*)(b + o_trav);
   d.n_trav = (int32_t)f.trav.size();
   d.strav = (const RtTrav*)(b + o_strav);
+  d.trav_c = (const RtTravC*)(b + o_travc);
+  d.strav_c = (const RtTravC*)(b + o_stravc);
   d.n_strav = (int32_t)f.strav.size();
   d.nodes = (const RtNode*)(b + o_nodes);
   d.leaves = (const RtLeaf*)(b + o_leaves);

@@ -155,6 +155,8 @@ struct DS {                         // device view of RtDevScene
   cptr<RtObject> objects;
   cptr<RtTrav> trav;
   cptr<RtTrav> strav;               // shadow-ray walk of scenes without a transparent object
+  cptr<RtTravC> trav_c;             // the same, compact (the generic walks with f32 culling)
+  cptr<RtTravC> strav_c;
   cptr<RtNode> nodes;
   cptr<RtLeaf> leaves;
   cptr<RtProg> prog;
@@ -558,8 +560,16 @@ __device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) 
 //  * the only infinite time that reaches the comparison is tn = +inf from such a zero component with
 //    the origin outside its slab (the ray never enters it: exact), and tf is finite (some component
 //    is >= 2^-10), so the slack never hides an infinity.
+// The specialised programs take it (4K globes 0.3184 -> 0.2868 ms); the generic kernels keep the f64
+// test: with f32 tests the generic walks of fractal.scene (171 objects, ray trees) ran the same
+// instructions and wave-cycles in 2.9x the time (its wavefront level-0 trace 0.59 -> 1.69 ms per
+// frame, profiles/r09p_*), and the generic 4K frame gained nothing (0.463 vs 0.457-0.487 ms).
 #ifndef RT_CULL_F32
+#ifdef RT_SPEC
 #define RT_CULL_F32 1
+#else
+#define RT_CULL_F32 0
+#endif
 #endif
 struct CullRayF { float ox, oy, oz, ix, iy, iz; };
 __device__ __forceinline__ float cull_rcp_f(float x) {
@@ -596,6 +606,23 @@ typedef double CullT;
 #define RT_CULL_TMAX(t) cull_tmax(t)
 #define RT_BOX_MAY_HIT(R, lo, hi, cr, tm) box_may_hit((R)->lo, (R)->hi, cr, tm)
 #endif
+// Hierarchy node accessors: the walks' lambdas take a node of either form -- RtTrav (the specialised
+// programs' constexpr tables, and f64-culling builds) or RtTravC (the generic walks with f32 culling).
+__device__ __forceinline__ int node_obj(cptr<RtTrav> T) { return T->obj; }
+__device__ __forceinline__ int node_skip(cptr<RtTrav> T) { return T->skip; }
+__device__ __forceinline__ int node_cull(cptr<RtTrav> T) { return T->cull; }
+__device__ __forceinline__ int node_shadow_skip(cptr<RtTrav> T) { return T->shadow_skip; }
+template <class CR, class TM> __device__ __forceinline__ bool node_may_hit(cptr<RtTrav> T, const CR& cr, TM tm) {
+  return RT_BOX_MAY_HIT(T, blo, bhi, cr, tm);
+}
+__device__ __forceinline__ int node_obj(cptr<RtTravC> T) { return T->obj; }
+__device__ __forceinline__ int node_skip(cptr<RtTravC> T) { return (int)(T->skip_flags & 0x0fffffffu); }
+__device__ __forceinline__ int node_cull(cptr<RtTravC> T) { return (int)((T->skip_flags >> 28) & 3u); }
+__device__ __forceinline__ int node_shadow_skip(cptr<RtTravC> T) { return (int)(T->skip_flags >> 30); }
+__device__ __forceinline__ bool node_may_hit(cptr<RtTravC> T, const CullRayF& cr, float tm) {
+  return fbox_may_hit(T->lo, T->hi, cr, tm);
+}
+
 // The range the host proves constant hit filters for (RtLeaf::filter_const): cull_ray's valid range
 // (origin within 1e6, largest direction component within [1e-100, 1e100]).
 __device__ __forceinline__ bool const_filter_range(V3 o, V3 d) {
@@ -675,16 +702,21 @@ __device__ __forceinline__ void walk_trav(const DS& S, G&& group, O&& object, bo
 #ifdef RT_SPEC
   spec_walk<SORD, 0, SORD ? rt_spec::N_STRAV : rt_spec::N_TRAV>(S, group, object);
 #else
+  // f32 culling: the compact nodes (RtTravC: two per scalar-cache line)
+#if RT_CULL_F32
+  const cptr<RtTravC> TR = SORD ? S.strav_c : S.trav_c;
+#else
   const cptr<RtTrav> TR = SORD ? S.strav : S.trav;
+#endif
   const int n_tr = SORD ? S.n_strav : S.n_trav;
   int resume = 0;
   for (int i = 0; i < n_tr;) {
-    cptr<RtTrav> T = &TR[i];
+    const auto T = &TR[i];
     const bool act = i >= resume;
-    if (T->obj < 0) {                                    // group node
+    if (node_obj(T) < 0) {                               // group node
       const bool in = act && group(T);
-      if (act && !in) resume = T->skip;
-      i = __ballot(in) ? i + 1 : T->skip;
+      if (act && !in) resume = node_skip(T);
+      i = __ballot(in) ? i + 1 : node_skip(T);
       continue;
     }
     ++i;
@@ -713,13 +745,13 @@ RT_FN int nearest_hit(const DS& S, V3 ro, V3 rd, double* dist) {
   // distance so far wins when its object comes earlier in DRAW order (o < bobj), which is the
   // reference's first-visited-wins rule (raytracer.rs:141-150) for any visiting order.
   constexpr bool NORDER = RT_NEAREST_ORDER && OBB;
-  auto group = [&](cptr<RtTrav> T) RT_INL { return RT_BOX_MAY_HIT(T, blo, bhi, cr, RT_CULL_TMAX(best)); };
-  auto object = [&](cptr<RtTrav> T) RT_INL {
+  auto group = [&](auto T) RT_INL { return node_may_hit(T, cr, RT_CULL_TMAX(best)); };
+  auto object = [&](auto T) RT_INL {
     // the object's cull kind and box come from the node's copy (RtTrav): one scalar load for the
     // node decides the common case; the object's own record is read only once its box passes
-    if (T->cull == RT_CULL_ALWAYS) return;
-    if (T->cull == RT_CULL_BOX && !RT_BOX_MAY_HIT(T, blo, bhi, cr, RT_CULL_TMAX(best))) return;
-    const int o = T->obj;
+    if (node_cull(T) == RT_CULL_ALWAYS) return;
+    if (node_cull(T) == RT_CULL_BOX && !node_may_hit(T, cr, RT_CULL_TMAX(best))) return;
+    const int o = node_obj(T);
     RT_REC(O, S, objects, OBJECTS, o);
     if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, ro, rd, RT_CULL_TMAX(best))) return;
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
@@ -767,12 +799,12 @@ RT_FN double shadow_transparency(const DS& S, V3 p, V3 dir, double dist) {
   const bool cf_ok = SHARE && RT_CONST_FILTER && const_filter_range(p, dir);
   const bool fin = wave_finite(p, dir);
   const CullT tmax = RT_CULL_TMAX(dist);
-  auto group = [&](cptr<RtTrav> T) RT_INL { return !done && RT_BOX_MAY_HIT(T, blo, bhi, cr, tmax); };
-  auto object = [&](cptr<RtTrav> T) RT_INL {
+  auto group = [&](auto T) RT_INL { return !done && node_may_hit(T, cr, tmax); };
+  auto object = [&](auto T) RT_INL {
     if (done) return;
-    if (T->shadow_skip || T->cull == RT_CULL_ALWAYS) return;     // the node's copies (see nearest_hit)
-    if (T->cull == RT_CULL_BOX && !RT_BOX_MAY_HIT(T, blo, bhi, cr, tmax)) return;
-    RT_REC(O, S, objects, OBJECTS, T->obj);
+    if (node_shadow_skip(T) || node_cull(T) == RT_CULL_ALWAYS) return;   // the node's copies (see nearest_hit)
+    if (node_cull(T) == RT_CULL_BOX && !node_may_hit(T, cr, tmax)) return;
+    RT_REC(O, S, objects, OBJECTS, node_obj(T));
     if (RT_OBB && OBB && O->obb_leaf >= 0 && !obb_may_hit(S, O, p, dir, tmax)) return;
     const double tobj = O->transparency;
     const int lb = O->leaf_begin, le = lb + O->leaf_count;
@@ -1510,6 +1542,8 @@ __device__ __forceinline__ DS make_ds(const RtDevScene& s) {
   d.n_trav = s.n_trav;
   d.strav = as_const(s.strav);
   d.n_strav = s.n_strav;
+  d.trav_c = as_const(s.trav_c);
+  d.strav_c = as_const(s.strav_c);
   d.nodes = as_const(s.nodes);
   d.leaves = as_const(s.leaves);
   d.prog = as_const(s.prog);
