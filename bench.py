@@ -60,6 +60,10 @@ CONFIGS = {
     "globes1080d5": ("globes", 1920, 1080, 0.0, 5),
     "sphere1080d0": (None, 1920, 1080, 0.0, 0),
 }
+# Default timed steps per config: a timed region of >= ~14 ms, as the headline's 50 x 0.27 ms.  The
+# sphere's 50 frames took 0.77 ms, in which the region's fixed cost (the synchronisations that bracket
+# it, ~35 us) was 5 % of the time (profiles/r09r_*: 50 steps 0.0154 ms/step, 1000 steps 0.0147).
+DEFAULT_STEPS = {"globes4k": 50, "globes1080d5": 200, "sphere1080d0": 1000, "anim120": 50}
 SPHERE_SCENE = "draw(sphere(<0, 0, 0>, 30, red))"      # BASELINE config 2
 # BASELINE config 5: the 120-frame spinning_globes animation at 1920x1080, time = f / 120,
 # frames dealt round-robin over the ranks (replicas, no collective).
@@ -69,7 +73,8 @@ ANIM = {"anim120": ("spinning_globes", 1920, 1080, 120, 10)}
 def parse():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: the config's DEFAULT_STEPS, a timed region of >= ~14 ms)")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="globes4k", choices=sorted(CONFIGS) + sorted(ANIM),
                     help="globes4k = the headline workload; anim120 = BASELINE config 5 (one step = the "
@@ -129,7 +134,10 @@ def parse():
     ap.add_argument("--launcher-check", action="store_true",
                     help="CPU/gloo check of the N-rank launcher, band layout, all-gather and assembly with a "
                          "synthetic pixel pattern (no GPU, no rendering, no measurement)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.steps is None:
+        a.steps = DEFAULT_STEPS.get(a.config, 50)
+    return a
 
 
 def _free_port() -> int:

@@ -82,6 +82,8 @@ def _lib(counting: bool = False):
     lib.orc_light.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
     lib.orc_texel_probe.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]
     lib.orc_texel_probe.restype = ctypes.c_int
+    lib.orc_hit_signature.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]
+    lib.orc_hit_signature.restype = ctypes.c_longlong
     lib.orc_get_pixel.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double,
                                   ctypes.POINTER(ctypes.c_double)]
     lib.orc_render_rows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -179,6 +181,12 @@ class OracleScene:
         out = (ctypes.c_double * 4)()
         o = self.lib.orc_texel_probe(self.h, float(x), float(y), out)
         return (o, tuple(out[:])) if o >= 0 else (-1, None)
+
+    def hit_signature(self, x: float, y: float) -> int:
+        """-1 for a miss, else object + 1 + 4096 * (bit i: light i's shadow ray occluded) of get_pixel(x, y)'s
+        primary hit: its changes along a line are silhouettes and shadow edges."""
+        t = ctypes.c_double(0.0)
+        return int(self.lib.orc_hit_signature(self.h, float(x), float(y), ctypes.byref(t)))
 
     def render(self, y0: int = 0, y1: int | None = None, row_step: int = 1, threads: int = 0,
                f64: bool = False, u8: bool = True):

@@ -1682,6 +1682,39 @@ int orc_texel_probe(const orc_scene *sc, double x, double y, double out[4]) {
   return (int)(obj - sc->objects);
 }
 
+/* Test infrastructure: get_pixel(x, y)'s primary hit (raytracer.rs:138-150) and, for each light, whether its
+ * shadow ray is occluded (transparency != 1, raytracer.rs:176-197) -- the signature whose changes along a
+ * scan line are the frame's silhouettes and shadow edges (tests/test_gpu_cull_edges.py bisects them).
+ * Returns -1 on a miss, else object + 1 + 4096 * (bit i: light i occluded); *t = the hit distance. */
+long long orc_hit_signature(const orc_scene *sc, double x, double y, double *t) {
+  Ray ray = camera_create_ray(&sc->camera, x, y);
+  NearestCtx nc = {INFINITY, NULL, NULL};
+  for (int i = 0; i < sc->n_objects; ++i) {
+    nc.cur = &sc->objects[i];
+    rtobject_intersects(&sc->objects[i], ray, add_nearest, &nc);
+  }
+  *t = nc.nearest;
+  if (!nc.nearest_obj) return -1;
+  Vec point = v_add(ray.point, v_scale(ray.direction, nc.nearest));
+  long long mask = 0;
+  for (int li = 0; li < sc->n_lights && li < 40; ++li) {
+    const PointLight *light = &sc->lights[li];
+    Ray shadow_ray;
+    shadow_ray.point = point;
+    shadow_ray.direction = v_normalized(v_sub(light->point, point));
+    ShadowCtx sh;
+    sh.distance = v_length(v_sub(light->point, point));
+    sh.transparency = 1.0;
+    sh.uv.u = sh.uv.v = 0.0;
+    for (int i = 0; i < sc->n_objects; ++i) {
+      sh.cached = &sc->objects[i];
+      rtobject_intersects(&sc->objects[i], shadow_ray, add_shadow, &sh);
+    }
+    if (sh.transparency != 1.0) mask |= 1ll << li;
+  }
+  return (long long)(nc.nearest_obj - sc->objects) + 1 + 4096 * mask;
+}
+
 typedef struct {
   const orc_scene *sc;
   int y0, y1, tid, nthreads, row_step;

@@ -1,0 +1,99 @@
+"""Exactness of the kernels' conservative culling at the edges it decides (rt_device.h fbox_may_hit).
+
+The specialised programs cull hierarchy nodes and leaves with f32 slab tests on outward-rounded boxes
+(scene.cpp f32_boxes); a box that an accepted hit lies in must never be culled.  The rays that come
+closest to a box's faces are the ones at an object's silhouette (an axis-aligned cube's box IS its
+surface, grown by RT_CULL32_MARGIN) and the shadow rays at a shadow's edge.  This test finds those
+rays on purpose: along scan lines it asks the oracle for the primary hit and which lights are occluded
+(orc_hit_signature, the reference's own nearest-hit and shadow loops, raytracer.rs:138-197), bisects
+every change of that signature down to adjacent doubles of the pixel coordinate, and renders those
+positions and their nearest neighbours through rt_render_points_f64 (get_pixel at fractional
+positions, antialiaser.rs:108-112).  Every point must give the oracle's RGBA8, and its f64 colour
+within 1e-9."""
+import math
+
+import numpy as np
+import pytest
+
+from tests.conftest import SCENES, scene_text
+
+pytestmark = pytest.mark.gpu
+
+# axis-aligned cubes (box == surface), a CSG intersection, a small sphere and two lights whose shadow
+# edges cross the floor and the cubes
+CUBES = (
+    "draw(plane(<0, 1, 0>, 25, rgb(0.5, 0.5, 0.5), 0.3))\n"
+    "draw(cube(<-30, -10, 10>, 14, red, 0.3))\n"
+    "draw(cube(<0, -15, 30>, 20, rgb(0.2, 0.8, 0.2), 0.5))\n"
+    "translate(25, -5, 0) draw(csg(cube(18), sphere(12), 'intersection', rgb(0.3, 0.3, 0.9), 0.4))\n"
+    "draw(sphere(<10, 10, -10>, 6, rgb(0.9, 0.9, 0.2), 0.2))\n"
+    "append light(<40, 60, -40>, white * 0.5, 100)\n"
+    "append light(<-50, 30, -20>, white * 0.4, 100)\n"
+    "set camera(<0, 10, -85>)\n"
+)
+
+
+def _u8(c):
+    """`(c * 255.0) as u8` (easy_pixbuf.rs:49-52) on an array: truncation, saturating, NaN -> 0."""
+    v = np.asarray(c, dtype=np.float64) * 255.0
+    with np.errstate(invalid="ignore"):
+        return np.where(~(v > 0.0), 0.0, np.where(v >= 255.0, 255.0, np.trunc(v))).astype(np.uint8)
+
+
+def _edges(osc, W, H, along_x, n_lines, step, cap):
+    """Adjacent-double pairs (lo, hi, c) of positions along scan lines where the hit signature changes."""
+    pairs = []
+    lines = np.linspace(0.07, 0.93, n_lines) * (H if along_x else W)
+    per_line = -(-cap // n_lines)
+    for c in lines:
+        n0, prev = len(pairs), None
+        for t in np.arange(0.5, (W if along_x else H) - 0.5, step):
+            x, y = (t, c) if along_x else (c, t)
+            cur = (t, osc.hit_signature(x, y))
+            if prev is not None and prev[1] != cur[1]:
+                lo, hi, s0 = prev[0], cur[0], prev[1]
+                while math.nextafter(lo, hi) != hi:
+                    mid = 0.5 * (lo + hi)
+                    if mid == lo or mid == hi:
+                        break
+                    xm, ym = (mid, c) if along_x else (c, mid)
+                    if osc.hit_signature(xm, ym) == s0:
+                        lo = mid
+                    else:
+                        hi = mid
+                pairs.append((lo, hi, c))
+                if len(pairs) >= cap:
+                    return pairs
+                if len(pairs) - n0 >= per_line:
+                    break
+            prev = cur
+    return pairs
+
+
+@pytest.mark.parametrize("name,W,H,depth", [("globes", 3840, 2160, 10), ("cubes", 1920, 1080, 10)])
+def test_silhouette_and_shadow_edges(worldmap, name, W, H, depth):
+    import tinyraytracerinrust_amd as T
+    from oracle import oracle as O
+    text = scene_text("globes") if name == "globes" else CUBES
+    osc = O.OracleScene(text, 0.0, W, H, max_depth=depth)
+    pts = []
+    for along_x in (True, False):
+        for lo, hi, c in _edges(osc, W, H, along_x, n_lines=80, step=2.0, cap=400):
+            ring = [lo, hi]
+            for _ in range(3):                                # 3 more doubles on each side
+                ring = [math.nextafter(ring[0], -math.inf)] + ring + [math.nextafter(ring[-1], math.inf)]
+            pts += [(t, c) if along_x else (c, t) for t in ring]
+    assert len(pts) >= 3200, len(pts)          # measured: globes 506 edges, cubes 558 (about half shadow edges)
+    xy = np.array(pts, dtype=np.float64)
+    r = T.Renderer(0)
+    r.upload(T.Scene.compile(text, 0.0, W, H, asset_dir=SCENES))
+    gpu = r.render_points(xy, max_depth=depth)
+    ref = np.array([osc.get_pixel(x, y) for x, y in pts])
+    g8, r8 = _u8(gpu[:, :3]), _u8(ref[:, :3])
+    bad = np.nonzero((g8 != r8).any(axis=1))[0]
+    d = np.abs(gpu - ref)
+    print(f"{name}: {len(pts)} points at {len(pts) // 8} silhouette / shadow edges (8 doubles around each); "
+          f"f64 bit-equal {100 * np.mean((gpu == ref).all(axis=1)):.2f} %, max |d| {np.nanmax(d):.3e}; "
+          f"RGBA8 mismatches {len(bad)}; kernel: {r.kernel_info() if hasattr(r, 'kernel_info') else '?'}")
+    assert len(bad) == 0, [(pts[i], g8[i].tolist(), r8[i].tolist(), osc.hit_signature(*pts[i])) for i in bad[:8]]
+    assert np.nanmax(d) <= 1e-9

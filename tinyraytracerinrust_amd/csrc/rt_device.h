@@ -560,6 +560,16 @@ __device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) 
 //  * the only infinite time that reaches the comparison is tn = +inf from such a zero component with
 //    the origin outside its slab (the ray never enters it: exact), and tf is finite (some component
 //    is >= 2^-10), so the slack never hides an infinity.
+// RT_CULL_FMA (a diagnostic variant, below): a slab time is one fma, fma(box, inv, -fl32(o * inv)) =
+// (box - o - o e1) inv (1 + e2), |e1|, |e2| <= 2^-24: the exact time of a ray from an origin moved by
+// |o e1| <= 2^16 * 2^-24 = 2^-8 on top of the f32 rounding (<= 2^-9), together under the margin, the
+// rest relative as above.  A component below 2^-100 then takes inv = +-2^100 (a direction of magnitude
+// 2^-100: over any t at which the ray can be in a finite box, t < 2^31 since every finite box and the
+// origin lie within 1e6 in EVERY axis (scene.cpp box_infinite), that moves the ray by < 2^-69), not
+// +-inf: fma(lo, inf, -o * inf) is NaN for the bound on one side of the origin and +-inf for the other,
+// and minNum(NaN, +inf) made +inf the near time of a ray parallel to a slab it starts inside
+// (tests/test_gpu_cull_edges.py found it: a shadow ray with d.x == 0 toward a light at the same x,
+// profiles/r09u_culldiff.txt).
 // The specialised programs take it (4K globes 0.3184 -> 0.2868 ms); the generic kernels keep the f64
 // test: with f32 tests the generic walks of fractal.scene (171 objects, ray trees) ran the same
 // instructions and wave-cycles in 2.9x the time (its wavefront level-0 trace 0.59 -> 1.69 ms per
@@ -571,22 +581,45 @@ __device__ __forceinline__ double cull_tmax(double t) { return t * (1.0 + 1e-7) 
 #define RT_CULL_F32 0
 #endif
 #endif
-struct CullRayF { float ox, oy, oz, ix, iy, iz; };
+// RT_CULL_FMA: each slab time as one fma (above) -- v_fmamk_f32 with the bound as its literal, one
+// instruction where (box - o) * inv takes two.  Conservative, and the
+// 4K kernel's VALU instructions per wave fell 1 174.6 -> 1 141.8, but every config ran slower (4K 0.2732
+// -> 0.2737 ms, sphere 0.0146 -> 0.0147, 1080p d5 0.0816 -> 0.0830; profiles/r09r_fma_slab_ab.txt):
+// kept as a diagnostic variant, off.
+#ifndef RT_CULL_FMA
+#define RT_CULL_FMA 0
+#endif
+#if RT_CULL_FMA
+struct CullRayF { float ix, iy, iz, nx, ny, nz; };   // 1 / d and -o / d (f32)
+#else
+struct CullRayF { float ix, iy, iz, ox, oy, oz; };
+#endif
 __device__ __forceinline__ float cull_rcp_f(float x) {
-  return fabsf(x) < 0x1p-100f ? copysignf(__builtin_inff(), x) : __builtin_amdgcn_rcpf(x);
+  return fabsf(x) < 0x1p-100f ? copysignf(RT_CULL_FMA ? 0x1p100f : __builtin_inff(), x) : __builtin_amdgcn_rcpf(x);
 }
 __device__ __forceinline__ CullRayF cull_ray_f(V3 o, V3 d) {
   const double ad = fmax(fmax(fabs(d.x), fabs(d.y)), fabs(d.z));
   const bool ok = fabs(o.x) <= RT_CULL32_COORD_MAX && fabs(o.y) <= RT_CULL32_COORD_MAX &&
                   fabs(o.z) <= RT_CULL32_COORD_MAX && ad >= 0x1p-10 && ad <= 0x1p10;
   const float nan = __builtin_nanf("");
-  return {(float)o.x, (float)o.y, (float)o.z, ok ? cull_rcp_f((float)d.x) : nan, ok ? cull_rcp_f((float)d.y) : nan,
-          ok ? cull_rcp_f((float)d.z) : nan};
+  const float ix = ok ? cull_rcp_f((float)d.x) : nan, iy = ok ? cull_rcp_f((float)d.y) : nan,
+              iz = ok ? cull_rcp_f((float)d.z) : nan;
+#if RT_CULL_FMA
+  return {ix, iy, iz, -((float)o.x * ix), -((float)o.y * iy), -((float)o.z * iz)};
+#else
+  return {ix, iy, iz, (float)o.x, (float)o.y, (float)o.z};
+#endif
 }
 template <class P> __device__ __forceinline__ bool fbox_may_hit(P lo, P hi, const CullRayF& r, float tmax) {
+#if RT_CULL_FMA
+  const float ax = __builtin_fmaf(lo[0], r.ix, r.nx), bx = __builtin_fmaf(hi[0], r.ix, r.nx);
+  const float ay = __builtin_fmaf(lo[1], r.iy, r.ny), by = __builtin_fmaf(hi[1], r.iy, r.ny);
+  const float az = __builtin_fmaf(lo[2], r.iz, r.nz), bz = __builtin_fmaf(hi[2], r.iz, r.nz);
+#else
   const float ax = (lo[0] - r.ox) * r.ix, bx = (hi[0] - r.ox) * r.ix;
   const float ay = (lo[1] - r.oy) * r.iy, by = (hi[1] - r.oy) * r.iy;
   const float az = (lo[2] - r.oz) * r.iz, bz = (hi[2] - r.oz) * r.iz;
+#endif
   const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
   const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
   return tn * (1.0f - 0x1p-18f) <= __builtin_fmaf(fabsf(tf), 0x1p-18f, tf);
@@ -703,7 +736,10 @@ __device__ __forceinline__ void walk_trav(const DS& S, G&& group, O&& object, bo
   spec_walk<SORD, 0, SORD ? rt_spec::N_STRAV : rt_spec::N_TRAV>(S, group, object);
 #else
   // f32 culling: the compact nodes (RtTravC: two per scalar-cache line)
-#if RT_CULL_F32
+#ifndef RT_TRAV_COMPACT
+#define RT_TRAV_COMPACT 1
+#endif
+#if RT_CULL_F32 && RT_TRAV_COMPACT
   const cptr<RtTravC> TR = SORD ? S.strav_c : S.trav_c;
 #else
   const cptr<RtTrav> TR = SORD ? S.strav : S.trav;
