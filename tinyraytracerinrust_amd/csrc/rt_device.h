@@ -333,6 +333,22 @@ RT_FN V3 leaf_normal(cptr<RtLeaf> L, V3 p, bool fin) {
 #ifndef RT_TEXEL_SAFE
 #define RT_TEXEL_SAFE 1
 #endif
+// The rare lanes' recomputation.  The specialised programs inline it (their guard costs 0.4 %); the
+// generic kernels call it: inlined at each of their shading sites, its double-double code made the
+// generic 4K frame 3.6x slower (0.430 -> 1.554 ms, profiles/r09v_generic_ab.txt).
+#ifdef RT_SPEC
+#define RT_TEXEL_CR_FN __device__ __forceinline__
+#else
+#define RT_TEXEL_CR_FN __device__ __attribute__((noinline))
+#endif
+RT_TEXEL_CR_FN void sphere_uv_cr(double cy, double cz, bool flip, double* u, double* v) {
+  double phi = rt_acos_cr(cy);                                             // rt_math.h
+  if (isnan(phi)) phi = 0.0;
+  double theta = rt_acos_cr(cz / rt_sin_cr(phi)) / (2.0 * PI_D);
+  if (isnan(theta)) theta = 0.0;
+  *v = phi / PI_D;
+  *u = flip ? 1.0 - theta : theta;
+}
 __device__ __forceinline__ double ulp_bound(double a) { return fabs(a) * 0x1p-52 + 0x1p-1074; }
 __device__ __forceinline__ bool near_int(double a, double m) { return !(fabs(a - rint(a)) > m); }   // NaN: near
 RT_FN void sphere_uv(cptr<RtLeaf> L, V3 p, double* u, double* v, int tw = 0, int th = 0) {
@@ -354,14 +370,8 @@ RT_FN void sphere_uv(cptr<RtLeaf> L, V3 p, double* u, double* v, int tw = 0, int
     const double er = 0x1p-50 + 4.0 * ulp_bound(phi) / fabs(sp);
     const double ea = fabs(r) * er / sqrt(fmax(1.0 - r * r, 0x1p-60)) + 2.0 * ulp_bound(ac);
     const double ex = (double)(tw - 1) * (ea / (2.0 * PI_D) + 2.0 * ulp_bound(*u)) + 2.0 * ulp_bound(x);
-    if (!(fabs(r) < 1.0 - 0x1p-26) || near_int(x, 16.0 * ex) || near_int(y, 16.0 * ey)) {
-      phi = rt_acos_cr(cy);                                                  // the rare lanes: rt_math.h
-      if (isnan(phi)) phi = 0.0;
-      theta = rt_acos_cr(cz / rt_sin_cr(phi)) / (2.0 * PI_D);
-      if (isnan(theta)) theta = 0.0;
-      *v = phi / PI_D;
-      *u = flip ? 1.0 - theta : theta;
-    }
+    if (!(fabs(r) < 1.0 - 0x1p-26) || near_int(x, 16.0 * ex) || near_int(y, 16.0 * ey))
+      sphere_uv_cr(cy, cz, flip, u, v);                                      // the rare lanes
   }
 }
 
