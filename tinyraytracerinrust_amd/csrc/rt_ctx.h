@@ -141,6 +141,7 @@ int wait_launches(rt_ctx* c);
 // spec.hip: the specialised programs of the uploaded scene -- flags (at upload, cheap), the request to the
 // compile pool (asynchronous), the load once compiled (at the next launch, or spec_wait), release
 void spec_flags(const FlatScene& f, rt_ctx* c);     // the scene's mode, clamp form, size limits
+bool same_structure_flat(const FlatScene& a, const FlatScene& b);   // spec.hip: a scene family's structure test
 void spec_prepare(rt_ctx* c, bool retry = false);   // request c's programs (spec_on, spec_flat); returns at once
 int spec_poll(rt_ctx* c);                           // load them if compiled: RT_OK, or RT_PENDING (spec_error on failure)
 int spec_wait(rt_ctx* c, double timeout_ms);        // block (< 0: no limit) then spec_poll

@@ -211,7 +211,13 @@ int rt_ctx_upload(rt_ctx* c, const rt_scene* s) {
     }
   }
   c->uploaded = true;
-  drop_orders(c);                     // tile costs belong to the previous scene
+  // Tile costs belong to the previous scene -- unless the new one has its structure (the same scene
+  // rebuilt, or the next frame of an animation: a host shaped like the reference's GUI rebuilds and
+  // uploads the scene every frame, debug_window.rs:53-68, gui.rs:78-89).  Then its orders stay: any
+  // tile order renders the same pixels, the old one is near the new costs, and the first launch after
+  // the upload takes an ordered (non-calibrating) kernel -- the specialised one, whose programs have no
+  // calibration variant at the default level (a calibrating launch would run the generic kernels).
+  if (!(c->spec_flat && rt::same_structure_flat(*c->spec_flat, f))) drop_orders(c);
   // the scene-specialised programs (spec.hip): requested from the compile pool, loaded by the first
   // launch after they are ready; the generic kernels render until then.  Only the flags are computed
   // here -- the program text (and a family lookup) only when the option is on and the scene fits.

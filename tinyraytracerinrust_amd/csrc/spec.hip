@@ -225,6 +225,8 @@ bool family_member(const SpecFamily& F, const rt::FlatScene& f) {
 
 namespace rt {
 
+bool same_structure_flat(const FlatScene& a, const FlatScene& b) { return same_structure(a, b); }
+
 // A diagnostic build's -D switches (Makefile: $(DIAG) as the string RT_SPEC_DIAG_DEFINES) as #define
 // lines for the programs' prelude, so the specialised kernels of a diagnostic build are built the way
 // its precompiled kernels are (empty in the product build).
