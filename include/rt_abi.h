@@ -155,8 +155,10 @@ int rt_ctx_upload(rt_ctx* ctx, const rt_scene* scene);
  * (written by the kernel on `stream`, asynchronously) or a host pointer (rendered into the
  * context's scratch and copied back; synchronous).  max_depth < 0 uses the scene's.
  * Tile order: the first launch of a row geometry (rows, bands, depth, f64) of >= 2048 8x8 tiles
- * on a context after rt_ctx_upload also records every tile's time and returns only after the
- * host has sorted the tiles (synchronous, once per geometry); later launches of that geometry
+ * on a context also records every tile's time and returns only after the host has sorted the
+ * tiles (synchronous, once per geometry; an rt_ctx_upload drops the orders unless the new scene
+ * has the previous one's structure -- the same scene rebuilt, an animation's next frame -- so a
+ * host that re-uploads every frame keeps them); later launches of that geometry
  * dispatch the costliest tiles first.  A context keeps the orders of its 8 most recently used
  * geometries; an order table is written once and never rewritten while launches on any stream
  * may read it.  Smaller launches are dispatched row-major.  The pixels are identical either
