@@ -70,12 +70,18 @@ def _edges(osc, W, H, along_x, n_lines, step, cap):
     return pairs
 
 
-@pytest.mark.parametrize("name,W,H,depth", [("globes", 3840, 2160, 10), ("cubes", 1920, 1080, 10)])
-def test_silhouette_and_shadow_edges(worldmap, name, W, H, depth):
+@pytest.mark.parametrize("name,t,W,H,depth", [
+    ("globes", 0.0, 3840, 2160, 10),            # the headline frame (reflection-only)
+    ("cubes", 0.0, 1920, 1080, 10),             # axis-aligned cubes: boxes that ARE the surfaces
+    ("spinning_globes", 0.5, 1920, 1080, 10),   # glass shells: the refraction walks (shared sphere terms)
+    ("three_cubes", 0.0, 1920, 1080, 10),       # rotated cubes: oriented object boxes
+    ("ground_star", 0.2, 1920, 1080, 10),
+])
+def test_silhouette_and_shadow_edges(worldmap, name, t, W, H, depth):
     import tinyraytracerinrust_amd as T
     from oracle import oracle as O
-    text = scene_text("globes") if name == "globes" else CUBES
-    osc = O.OracleScene(text, 0.0, W, H, max_depth=depth)
+    text = CUBES if name == "cubes" else scene_text(name)
+    osc = O.OracleScene(text, t, W, H, max_depth=depth)
     pts = []
     for along_x in (True, False):
         for lo, hi, c in _edges(osc, W, H, along_x, n_lines=80, step=2.0, cap=400):
@@ -83,10 +89,12 @@ def test_silhouette_and_shadow_edges(worldmap, name, W, H, depth):
             for _ in range(3):                                # 3 more doubles on each side
                 ring = [math.nextafter(ring[0], -math.inf)] + ring + [math.nextafter(ring[-1], math.inf)]
             pts += [(t, c) if along_x else (c, t) for t in ring]
-    assert len(pts) >= 3200, len(pts)          # measured: globes 506 edges, cubes 558 (about half shadow edges)
+    # measured: globes 506 edges, cubes 558 (about half shadow edges), spinning_globes 369, three_cubes 591,
+    # ground_star 482
+    assert len(pts) >= 2400, len(pts)
     xy = np.array(pts, dtype=np.float64)
     r = T.Renderer(0)
-    r.upload(T.Scene.compile(text, 0.0, W, H, asset_dir=SCENES))
+    r.upload(T.Scene.compile(text, t, W, H, asset_dir=SCENES))
     gpu = r.render_points(xy, max_depth=depth)
     ref = np.array([osc.get_pixel(x, y) for x, y in pts])
     g8, r8 = _u8(gpu[:, :3]), _u8(ref[:, :3])
