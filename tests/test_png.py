@@ -67,3 +67,24 @@ def test_corrupt_png_errors(tmp_path):
         T.read_png_rgba8(str(p))
     with pytest.raises(T.RtError):
         T.read_png_rgba8(str(tmp_path / "missing.png"))
+
+
+def test_scene_texture_cache_keyed_by_file_content(tmp_path):
+    """The scene compiler keeps decoded textures by the PNG file's bytes (scene_dsl.cpp decoded_png): a
+    scene rebuilt from an unchanged file reuses the pixels, a rewritten file under the same name gives
+    the new image (its size shows in the scene's specialised program text, which holds the texture
+    records)."""
+    from PIL import Image
+    import tinyraytracerinrust_amd as T
+    text = 'draw(sphere(<0, 0, 0>, 20, texture("tex.png")))'
+    rng = np.random.default_rng(3)
+    Image.fromarray(rng.integers(0, 256, (4, 6, 4), dtype=np.uint8), "RGBA").save(tmp_path / "tex.png")
+    a1 = T.Scene.compile(text, 0.0, 32, 24, asset_dir=str(tmp_path)).spec_program()
+    a2 = T.Scene.compile(text, 0.0, 32, 24, asset_dir=str(tmp_path)).spec_program()
+    assert a1 == a2
+    Image.fromarray(rng.integers(0, 256, (9, 5, 4), dtype=np.uint8), "RGBA").save(tmp_path / "tex.png")
+    b = T.Scene.compile(text, 0.0, 32, 24, asset_dir=str(tmp_path)).spec_program()
+    assert b != a1
+    Image.fromarray(rng.integers(0, 256, (4, 6, 4), dtype=np.uint8), "RGBA").save(tmp_path / "tex.png")
+    c = T.Scene.compile(text, 0.0, 32, 24, asset_dir=str(tmp_path)).spec_program()
+    assert c == a1                    # same size again (new pixels live in the scene's texels, not the text)

@@ -11,6 +11,7 @@
 
 #include <array>
 #include <map>
+#include <mutex>
 #include <stdexcept>
 #include <memory>
 #include <string>
@@ -20,6 +21,45 @@
 
 namespace rt {
 namespace {
+
+// Decoded textures, process-wide, keyed by the PNG file's bytes (a 64-bit FNV-1a and the size, then the
+// bytes compared in full): a hit is the same file content, so the same pixels.  At most 8 images are
+// kept (least recently used dropped).
+struct DecodedPng {
+  std::vector<uint8_t> file;
+  std::vector<uint8_t> rgba;
+  uint32_t w = 0, h = 0;
+  uint64_t last_use = 0;
+};
+std::shared_ptr<const DecodedPng> decoded_png(const std::vector<uint8_t>& file) {
+  static std::mutex mu;
+  static std::map<std::pair<uint64_t, size_t>, std::shared_ptr<DecodedPng>> cache;
+  static uint64_t clock = 0;
+  uint64_t hsh = 1469598103934665603ull;
+  for (uint8_t b : file) hsh = (hsh ^ b) * 1099511628211ull;
+  const auto key = std::make_pair(hsh, file.size());
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end() && it->second->file == file) {
+      it->second->last_use = ++clock;
+      return it->second;
+    }
+  }
+  auto img = std::make_shared<DecodedPng>();
+  if (png_decode_rgba8(file, &img->rgba, &img->w, &img->h)) return nullptr;
+  img->file = file;
+  std::lock_guard<std::mutex> lk(mu);
+  img->last_use = ++clock;
+  if (cache.size() >= 8 && !cache.count(key)) {
+    auto lru = cache.begin();
+    for (auto it = cache.begin(); it != cache.end(); ++it)
+      if (it->second->last_use < lru->second->last_use) lru = it;
+    cache.erase(lru);
+  }
+  cache[key] = img;
+  return img;
+}
 
 // ------------------------------------------------------------------ values (value.rs:5-14)
 struct DslShape;
@@ -773,17 +813,18 @@ class Evaluator {
     if (rc) throw EvalError{rc, rt_last_error()};
   }
 
-  // Texture::from_file (sceneparser/texture.rs:20-40), path relative to asset_dir
+  // Texture::from_file (sceneparser/texture.rs:20-40), path relative to asset_dir.  The file is read
+  // every time (as the reference reads it); its decoded pixels come from decoded_png, keyed by the file's
+  // bytes, so a host that rebuilds the scene every frame (debug_window.rs:53-68) decodes it once.
   int32_t load_texture(const std::string& name) {
     auto c = texture_cache_.find(name);
     if (c != texture_cache_.end()) return c->second;
     std::string path = (asset_dir_.empty() || name.empty() || name[0] == '/') ? name : asset_dir_ + "/" + name;
-    std::vector<uint8_t> file, rgba;
+    std::vector<uint8_t> file;
     if (!read_file(path, &file)) throw EvalError{RT_ERR_IO, "cannot read texture " + path};
-    uint32_t w = 0, h = 0;
-    int rc = png_decode_rgba8(file, &rgba, &w, &h);
-    if (rc) throw EvalError{RT_ERR_IO, std::string("cannot decode texture ") + path + ": " + rt_last_error()};
-    int id = rt_scene_add_texture(sc_, w, h, rgba.data());
+    std::shared_ptr<const DecodedPng> img = decoded_png(file);
+    if (!img) throw EvalError{RT_ERR_IO, std::string("cannot decode texture ") + path + ": " + rt_last_error()};
+    int id = rt_scene_add_texture(sc_, img->w, img->h, img->rgba.data());
     if (id < 0) throw EvalError{id, rt_last_error()};
     texture_cache_[name] = id;
     return id;
